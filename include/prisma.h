@@ -1,0 +1,236 @@
+/*
+ * prisma.h — C-ABI of the MI355X-native PRISMA packet-hop engine.
+ *
+ * One shared library (libprisma_amd.so, built from prisma_amd/csrc/) holds
+ * R independent topology replicas of PRISMA's ns-3 routing scenario as
+ * structure-of-arrays state in HBM and advances them with hand-written
+ * gfx950 kernels.  Plain C types only: pointers, sizes, status codes.
+ * Device pointers are HIP device addresses (e.g. torch.Tensor.data_ptr()).
+ *
+ * Each entry point replaces one piece of the reference's per-node
+ * ns3-gym path (all citations relative to the reference repo root):
+ *
+ *   prisma_create      sim.cc:274-683 (topology, links, flows, per-node envs)
+ *                      + ns3env.py:378-403 (Ns3Env.__init__ / SimInitMsg)
+ *   prisma_reset       sim.cc:253-261 (SetSeed/SetRun) + Simulator start,
+ *                      ns3env.py:426-445 (Ns3Env.reset)
+ *   prisma_step        ns3env.py:420-423 (Ns3Env.step) ==
+ *                      packet-routing-gym.cc:197-213 (ExecuteActions) then
+ *                      Simulator::Run until the next
+ *                      packet-routing-gym.cc:231-267 (NotifyPktRcv -> Notify)
+ *                      with the observation of data-packet-manager.cc:171-206
+ *   prisma_run         the same loop with the forwarding decision fused
+ *                      in-kernel (forwarder.py:149-195 for table policies:
+ *                      SP next-hop table, DQ-routing argmin table)
+ *   prisma_read_counters  compute-stats-v2.cc:87-266 (ComputeStats) and the
+ *                      forwarder.py:308-431 per-episode trackers
+ *   prisma_log_view    the per-hop replay transitions of forwarder.py:352-379
+ *                      and the loss transitions of forwarder.py:214-244
+ *   prisma_destroy     ns3env.py:452-455 (Ns3Env.close) /
+ *                      Ns3ZmqBridge.send_close_command
+ *
+ * Error behaviour: every call returns PRISMA_OK (0) or a negative status;
+ * prisma_last_error() returns a static description of the last failure in
+ * the calling thread.  The library never calls exit() (the reference
+ * NS_FATAL_ERRORs on bad matrices, sim.cc:310-313; here that is
+ * PRISMA_ERR_CONFIG).  Per-replica runtime faults (a ring or wire overflow
+ * that the host-side sizing should have excluded) set bits in
+ * prisma_counters_t.error and stop that replica; they never touch memory
+ * outside the replica's own state.
+ */
+#ifndef PRISMA_AMD_PRISMA_H
+#define PRISMA_AMD_PRISMA_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PRISMA_ABI_VERSION 1
+
+/* status codes */
+#define PRISMA_OK              0
+#define PRISMA_ERR_CONFIG     -1   /* invalid topology / parameters        */
+#define PRISMA_ERR_NOMEM      -2   /* hipMalloc failed                     */
+#define PRISMA_ERR_DEVICE     -3   /* no HIP device / wrong architecture   */
+#define PRISMA_ERR_LAUNCH     -4   /* kernel launch failed                 */
+#define PRISMA_ERR_ARG        -5   /* null handle / bad pointer / bad size */
+#define PRISMA_ERR_STATE      -6   /* call not valid in current state      */
+
+/* policy modes for prisma_run (fused decision) */
+#define PRISMA_POLICY_TABLE    1   /* action = table[node * n_nodes + dst] */
+
+/* per-decision status (prisma_record_t.status) */
+#define PRISMA_ST_PENDING      0   /* waiting for an action (prisma_step)  */
+#define PRISMA_ST_ENQUEUED     1   /* forwarded; a later record has prev==d */
+#define PRISMA_ST_DROPPED      2   /* output FIFO overflow: loss transition */
+#define PRISMA_ST_DESTINATION  3   /* packet reached its destination       */
+#define PRISMA_ST_DISCARDED    4   /* action >= degree: silently discarded  */
+
+/* runtime error bits (prisma_counters_t.error) */
+#define PRISMA_EBIT_RING       1u  /* link ring overflow                   */
+#define PRISMA_EBIT_WIRE       2u  /* more packets on a wire than sized    */
+#define PRISMA_EBIT_ACKORDER   4u  /* ping-back arrived out of order       */
+#define PRISMA_EBIT_TIME       8u  /* time beyond the representable range  */
+
+/*
+ * Topology of one replica (identity overlay: every underlay node is an
+ * overlay node, overlay adjacency == physical adjacency).  Directed
+ * switch links are numbered in CSR order: links row_ptr[u] ..
+ * row_ptr[u+1]-1 leave node u towards link_dst[] in ascending neighbour
+ * id, which is the action order of the reference (sim.cc:469-476,
+ * forwarder.py:191).  link_rev[l] is the opposite direction of l.
+ * Flows are listed in (src, dst) lexicographic order with their
+ * load-scaled integer bit rate ceil(trunc_parse(TM[s][d]) * load_factor)
+ * (sim.cc:599-631, ns-3 DataRate parse).
+ */
+typedef struct prisma_topology {
+    int32_t n_nodes;
+    int32_t n_links;            /* directed switch links E                 */
+    int32_t n_flows;
+    int32_t max_deg;
+    const int32_t*  row_ptr;    /* [n_nodes + 1]                           */
+    const int32_t*  link_dst;   /* [n_links]                               */
+    const int32_t*  link_rev;   /* [n_links]                               */
+    const int32_t*  flow_src;   /* [n_flows]                               */
+    const int32_t*  flow_dst;   /* [n_flows]                               */
+    const uint64_t* flow_rate_bps; /* [n_flows], > 0                       */
+} prisma_topology_t;
+
+/* scenario parameters (argument_parser.py:34-94 defaults in brackets) */
+typedef struct prisma_params {
+    uint64_t link_bps;          /* switch link rate            [500000]    */
+    int64_t  link_delay_ns;     /* propagation delay           [1 ms]      */
+    uint32_t max_buffer_bytes;  /* DropTail byte limit         [16260]     */
+    uint32_t packet_size;       /* UDP payload bytes           [512]       */
+    double   sim_time_s;        /* episode length              [60]        */
+    float    ping_interval_s;   /* pingPacketIntervalTime      [0.2f]      */
+    uint32_t ma_size;           /* movingAverageObsSize        [5]         */
+    uint32_t ping_as_obs;       /* pingAsObs                   [1]         */
+    uint32_t auto_reset;        /* start next episode when one ends        */
+    double   loss_penalty;      /* ((16260+542)*8/cap+0.001)*N             */
+    uint64_t seed;              /* simSeed                     [100]       */
+    uint32_t replica_base;      /* global id of replica 0 (multi-GPU)      */
+    uint32_t log_capacity;      /* records kept per replica (power of 2)   */
+} prisma_params_t;
+
+/*
+ * One decision record = one data-packet notification of the reference
+ * (PacketRoutingEnv::Notify for a valid DATA packet), i.e. one row the
+ * reference Forwarder turns into a replay transition.  The transition of
+ * decision d is (obs_d, action_d, r, obs_{d'}, done_{d'}) where d' is the
+ * record with prev == d and r = reward_{d'}; or, if status_d == DROPPED,
+ * (obs_d, action_d, loss_penalty, [dst, 0...], true) (forwarder.py:226-240).
+ * reward is the reference's hop_time_real = curr_time - t_decision computed
+ * on the microsecond-formatted times (packet-manager.cc:127-128 ->
+ * forwarder.py:208,360), bit-identical to the Python float.
+ * Record size is 32 + 4 * obs_width bytes (obs_width = 1 + max_deg rounded
+ * up to even).
+ */
+typedef struct prisma_record {
+    int64_t  t_ns;
+    double   reward;
+    uint32_t uid;
+    int32_t  prev;
+    uint16_t node;
+    uint16_t dst;
+    int8_t   action;
+    uint8_t  status;
+    uint16_t episode;
+    uint32_t obs[];             /* [obs_width]                             */
+} prisma_record_t;
+
+/* Per-replica counters: ComputeStats (compute-stats-v2.cc) + engine stats */
+typedef struct prisma_counters {
+    uint64_t events;            /* discrete events executed                */
+    uint64_t hops;              /* decisions resulting in enqueue or drop  */
+    uint64_t decisions;         /* all data notifications (incl. dest)     */
+    uint64_t hop_deg_sum;       /* sum of deg(u) over executed hops        */
+    int64_t  now_ns;            /* simulation clock                        */
+    double   reward_sum;        /* sum of completed hop rewards + penalties*/
+    int32_t  ov_injected;       /* compute-stats-v2.cc:131-134             */
+    int32_t  ov_arrived;
+    int32_t  ov_lost;
+    int32_t  un_injected;
+    int32_t  un_arrived;
+    int32_t  un_lost;
+    int32_t  bytes_data;        /* addGlobalBytesData                      */
+    int32_t  bytes_signaling;   /* addGlobalBytesSignaling                 */
+    float    cost_sum;          /* running float sum of m_globalCost       */
+    float    e2e_sum;           /* running float sum of m_globalE2eDelay   */
+    int32_t  cost_n;
+    int32_t  e2e_n;
+    uint32_t episode;
+    uint32_t ping_rounds;
+    uint32_t seq;               /* events scheduled (ns-3 uid analogue)    */
+    uint32_t uid;               /* data packets created                    */
+    uint32_t dec_count;         /* records written (monotonic)             */
+    uint32_t ctrl_dropped;      /* ping packets lost on full FIFOs         */
+    uint32_t error;             /* PRISMA_EBIT_* bits                      */
+    uint32_t episode_over;      /* 1 once the current episode ended        */
+    uint64_t hops_total;        /* hops over all episodes since reset      */
+    uint64_t events_total;      /* events over all episodes since reset    */
+} prisma_counters_t;
+
+/* library-owned device buffers (valid until prisma_destroy) */
+typedef struct prisma_log_view {
+    void*     records;          /* [n_replicas][log_capacity] records      */
+    uint32_t  record_bytes;
+    uint32_t  log_capacity;
+    int32_t   obs_width;
+    int32_t   n_replicas;
+} prisma_log_view_t;
+
+typedef struct prisma_env prisma_env_t;
+
+int         prisma_abi_version(void);
+const char* prisma_last_error(void);
+
+/* Size the per-replica state for this topology and allocate it on
+ * `device`.  Validates shapes and ids up front. */
+int prisma_create(const prisma_topology_t* topo, const prisma_params_t* params,
+                  int32_t n_replicas, int32_t device, prisma_env_t** out);
+
+/* Start episode `episode` of every replica (replica r uses Philox key
+ * (seed, replica_base + r)).  Asynchronous on `stream` (hipStream_t). */
+int prisma_reset(prisma_env_t* env, uint32_t episode, void* stream);
+
+/* Apply one action per replica to its pending decision (actions may be
+ * NULL on the first call after reset), then advance every replica to its
+ * next pending decision.  obs_out: device int32 [n_replicas][obs_width];
+ * mask_out: device uint8 [n_replicas] (1 = a decision is pending, 0 =
+ * episode over).  Either output may be NULL. */
+int prisma_step(prisma_env_t* env, const int32_t* actions, int32_t* obs_out,
+                uint8_t* mask_out, void* stream);
+
+/* Fused policy: advance every replica by up to max_hops hops, deciding
+ * in-kernel with `table` (device uint8 [n_nodes][n_nodes] action table). */
+int prisma_run(prisma_env_t* env, int32_t policy, const uint8_t* table,
+               int32_t max_hops, void* stream);
+
+/* Copy per-replica counters (n_replicas entries) to host memory.
+ * Synchronises `stream`. */
+int prisma_read_counters(prisma_env_t* env, prisma_counters_t* host_out,
+                         void* stream);
+
+/* Device pointer to the per-replica counters array (prisma_counters_t
+ * [n_replicas]), for device-side reductions / collectives. */
+int prisma_counters_device(prisma_env_t* env, void** dev_ptr);
+
+int prisma_log_view(prisma_env_t* env, prisma_log_view_t* out);
+
+/* Device-to-device copy of the whole log ring ([n_replicas][log_capacity]
+ * records) into caller memory of at least `bytes` bytes, on `stream`. */
+int prisma_copy_log(prisma_env_t* env, void* dst_device, uint64_t bytes, void* stream);
+
+/* Bytes of per-replica state (the LDS image) and LDS bytes per workgroup. */
+int prisma_state_bytes(prisma_env_t* env, uint32_t* state_bytes,
+                       uint32_t* lds_bytes);
+
+void prisma_destroy(prisma_env_t* env);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PRISMA_AMD_PRISMA_H */

@@ -1,0 +1,176 @@
+"""ctypes binding of the CPU oracle — TEST INFRASTRUCTURE ONLY.
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg (as the parity checker / CPU baseline), never from the
+prisma_amd package.  See oracle/prisma_oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_build", "liboracle.so")
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(HERE, "prisma_oracle.c")
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["make", "-s", "-C", HERE])
+    return LIB_PATH
+
+
+class OrConfig(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_int32), ("n_links", C.c_int32), ("n_flows", C.c_int32), ("max_deg", C.c_int32),
+        ("row_ptr", C.POINTER(C.c_int32)), ("link_dst", C.POINTER(C.c_int32)),
+        ("link_rev", C.POINTER(C.c_int32)), ("flow_src", C.POINTER(C.c_int32)),
+        ("flow_dst", C.POINTER(C.c_int32)), ("flow_rate_bps", C.POINTER(C.c_uint64)),
+        ("link_bps", C.c_uint64), ("link_delay_ns", C.c_int64), ("max_buffer_bytes", C.c_uint32),
+        ("packet_size", C.c_uint32), ("sim_time_s", C.c_double), ("ping_interval_s", C.c_float),
+        ("ma_size", C.c_uint32), ("ping_as_obs", C.c_uint32), ("auto_reset", C.c_uint32),
+        ("loss_penalty", C.c_double), ("seed", C.c_uint64), ("replica", C.c_uint32),
+        ("episode", C.c_uint32),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = C.CDLL(LIB_PATH)
+        L.or_create.restype = C.c_void_p
+        L.or_create.argtypes = [C.POINTER(OrConfig)]
+        L.or_destroy.argtypes = [C.c_void_p]
+        L.or_step.restype = C.c_int
+        L.or_step.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
+        L.or_run_table.restype = C.c_int64
+        L.or_run_table.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.or_record_count.restype = C.c_int64
+        L.or_record_count.argtypes = [C.c_void_p]
+        L.or_obs_width.restype = C.c_int32
+        L.or_obs_width.argtypes = [C.c_void_p]
+        L.or_copy_records.restype = C.c_int64
+        L.or_copy_records.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
+        L.or_counters.argtypes = [C.c_void_p, C.c_void_p]
+        L.or_enable_trace.argtypes = [C.c_void_p, C.c_int]
+        L.or_trace_count.restype = C.c_int64
+        L.or_trace_count.argtypes = [C.c_void_p]
+        L.or_copy_trace.restype = C.c_int64
+        L.or_copy_trace.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
+        L.or_last_info.restype = C.c_int32
+        L.or_last_info.argtypes = [C.c_void_p, C.c_char_p, C.c_int32]
+        L.or_philox4x32_10.argtypes = [C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+        L.or_det_log.restype = C.c_double
+        L.or_det_log.argtypes = [C.c_double]
+        L.or_seconds_to_ns.restype = C.c_int64
+        L.or_seconds_to_ns.argtypes = [C.c_double]
+        L.or_py_micros.restype = C.c_uint64
+        L.or_py_micros.argtypes = [C.c_int64]
+        _lib = L
+    return _lib
+
+
+def philox(ctr, key):
+    c = (C.c_uint32 * 4)(*ctr)
+    k = (C.c_uint32 * 2)(*key)
+    o = (C.c_uint32 * 4)()
+    lib().or_philox4x32_10(c, k, o)
+    return list(o)
+
+
+class OracleSim:
+    """One replica of the scenario on the CPU (literal heap-based DES)."""
+
+    def __init__(self, topo, params: dict, replica: int = 0, episode: int = 0):
+        from prisma_amd.records import record_dtype, COUNTERS_DTYPE  # layout only
+        self.topo = topo
+        self._keep = []
+
+        def arr(a, ct, dt):
+            a = np.ascontiguousarray(a, dtype=dt)
+            self._keep.append(a)
+            return a.ctypes.data_as(C.POINTER(ct))
+
+        cfg = OrConfig()
+        cfg.n_nodes = topo.n_nodes
+        cfg.n_links = topo.n_links
+        cfg.n_flows = topo.n_flows
+        cfg.max_deg = topo.max_deg
+        cfg.row_ptr = arr(topo.row_ptr, C.c_int32, np.int32)
+        cfg.link_dst = arr(topo.link_dst, C.c_int32, np.int32)
+        cfg.link_rev = arr(topo.link_rev, C.c_int32, np.int32)
+        cfg.flow_src = arr(topo.flow_src, C.c_int32, np.int32)
+        cfg.flow_dst = arr(topo.flow_dst, C.c_int32, np.int32)
+        cfg.flow_rate_bps = arr(topo.flow_rate_bps, C.c_uint64, np.uint64)
+        cfg.link_bps = int(params["link_bps"])
+        cfg.link_delay_ns = int(params["link_delay_ns"])
+        cfg.max_buffer_bytes = int(params["max_buffer_bytes"])
+        cfg.packet_size = int(params["packet_size"])
+        cfg.sim_time_s = float(params["sim_time_s"])
+        cfg.ping_interval_s = float(params["ping_interval_s"])
+        cfg.ma_size = int(params["ma_size"])
+        cfg.ping_as_obs = int(params["ping_as_obs"])
+        cfg.auto_reset = 0
+        cfg.loss_penalty = float(params["loss_penalty"])
+        cfg.seed = int(params["seed"])
+        cfg.replica = int(replica)
+        cfg.episode = int(episode)
+        self._cfg = cfg
+        self.W = topo.obs_width
+        self.rec_dtype = record_dtype(self.W)
+        self.cnt_dtype = COUNTERS_DTYPE
+        self.h = lib().or_create(C.byref(cfg))
+
+    def close(self):
+        if self.h:
+            lib().or_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def step(self, action: int = -1):
+        obs = np.zeros(self.W, dtype=np.int32)
+        r = lib().or_step(self.h, int(action), obs.ctypes.data)
+        return (obs if r else None)
+
+    def run_table(self, table: np.ndarray, max_hops: int) -> int:
+        t = np.ascontiguousarray(table, dtype=np.uint8)
+        return int(lib().or_run_table(self.h, t.ctypes.data, int(max_hops)))
+
+    def records(self, first: int = 0, count: int = None) -> np.ndarray:
+        n = int(lib().or_record_count(self.h))
+        if count is None:
+            count = n - first
+        out = np.zeros(max(count, 0), dtype=self.rec_dtype)
+        got = lib().or_copy_records(self.h, int(first), int(count), out.ctypes.data)
+        return out[:got]
+
+    def counters(self) -> np.ndarray:
+        out = np.zeros(1, dtype=self.cnt_dtype)
+        lib().or_counters(self.h, out.ctypes.data)
+        return out[0]
+
+    def enable_trace(self, on: bool = True):
+        lib().or_enable_trace(self.h, int(on))
+
+    def trace(self) -> np.ndarray:
+        n = int(lib().or_trace_count(self.h))
+        out = np.zeros((n, 4), dtype=np.int64)
+        lib().or_copy_trace(self.h, 0, n, out.ctypes.data)
+        return out
+
+    def last_info(self) -> str:
+        buf = C.create_string_buffer(8192)
+        lib().or_last_info(self.h, buf, 8192)
+        return buf.value.decode()

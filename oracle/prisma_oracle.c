@@ -1,0 +1,784 @@
+/*
+ * prisma_oracle.c — TEST INFRASTRUCTURE ONLY (see prisma_oracle.h).
+ *
+ * Literal single-replica restatement of the reference's ns-3 scenario for
+ * identity overlays.  Every handler cites the reference callback it
+ * restates (paths relative to the reference root, prisma/ns3/ unless
+ * noted).  ns-3 upstream semantics that are not in the reference tree are
+ * stated from the ns-3 API:
+ *   - Time is int64 nanoseconds; Seconds(x) is restated as
+ *     (int64)(x * 1e9 + 0.5) for x >= 0 (round-to-nearest);
+ *   - Time::GetSeconds() is restated as (double)t / 1e9;
+ *   - DataRate::CalculateBytesTxTime(b) = Seconds((double)b * 8 / bps);
+ *   - byte-mode Queue::DoEnqueue drops iff nbytes + size > max;
+ *   - PointToPointChannel delivers at start + txTime + delay;
+ *   - the scheduler runs events in (time, insertion uid) order.
+ * RNG: ns-3's MRG32k3a streams are replaced by a counter-based
+ * Philox4x32-10 (Salmon et al., SC'11 / Random123), keyed by
+ * (seed, replica) with counter (flow, draw, episode, purpose); parity with
+ * real ns-3 draws is unpinned.
+ *
+ * Build: cc -O2 -std=c11 -ffp-contract=off -fPIC -shared (oracle/Makefile).
+ */
+#include "prisma_oracle.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------ */
+/* RNG + numeric helpers                                               */
+/* ------------------------------------------------------------------ */
+void or_philox4x32_10(const uint32_t ctr_in[4], const uint32_t key_in[2], uint32_t out[4]) {
+    uint32_t c0 = ctr_in[0], c1 = ctr_in[1], c2 = ctr_in[2], c3 = ctr_in[3];
+    uint32_t k0 = key_in[0], k1 = key_in[1];
+    for (int round = 0; round < 10; ++round) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * (uint64_t)c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * (uint64_t)c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0;
+        uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* Natural log by range reduction + atanh series; only + - * / so the
+ * result is identical on every IEEE-754 double implementation. */
+double or_det_log(double x) {
+    uint64_t bits;
+    memcpy(&bits, &x, 8);
+    int e = (int)((bits >> 52) & 0x7ff) - 1023;
+    bits = (bits & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL;
+    double m;
+    memcpy(&m, &bits, 8);
+    if (m > 1.4142135623730951) { m = m * 0.5; e += 1; }
+    double f = m - 1.0;
+    double s = f / (2.0 + f);
+    double z = s * s;
+    double p = 2.0 / 19.0;
+    p = p * z + 2.0 / 17.0;
+    p = p * z + 2.0 / 15.0;
+    p = p * z + 2.0 / 13.0;
+    p = p * z + 2.0 / 11.0;
+    p = p * z + 2.0 / 9.0;
+    p = p * z + 2.0 / 7.0;
+    p = p * z + 2.0 / 5.0;
+    p = p * z + 2.0 / 3.0;
+    double logm = 2.0 * s + s * (z * p);
+    double de = (double)e;
+    return de * 6.93147180369123816490e-01 + (de * 1.90821492927058770002e-10 + logm);
+}
+
+int64_t or_seconds_to_ns(double s) { return (int64_t)(s * 1e9 + 0.5); }
+
+static double get_seconds(int64_t t) { return (double)t / 1e9; }
+
+/* Microseconds that Python reads back from std::to_string(GetSeconds())
+ * ("%f": the double rounded to 6 decimals, ties to even on the exact
+ * binary value) — packet-manager.cc:127-128 -> forwarder.py:208. */
+uint64_t or_py_micros(int64_t t) {
+    uint64_t u = (uint64_t)(t / 1000);
+    int64_t r = t % 1000;
+    if (r < 500) return u;
+    if (r > 500) return u + 1;
+    double x = get_seconds(t);
+    uint64_t b;
+    memcpy(&b, &x, 8);
+    int ex = (int)((b >> 52) & 0x7ff);
+    uint64_t mant = b & 0x000fffffffffffffULL;
+    if (ex == 0) ex = 1; else mant |= 0x0010000000000000ULL;
+    int sh = -(ex - 1075);               /* x = mant * 2^-(sh) */
+    unsigned __int128 lhs = (unsigned __int128)mant * 2000000u;
+    unsigned __int128 rhs = (unsigned __int128)(2 * u + 1);
+    if (sh >= 0) rhs <<= sh; else lhs <<= -sh;
+    if (lhs > rhs) return u + 1;
+    if (lhs < rhs) return u;
+    return (u & 1) ? u + 1 : u;
+}
+
+static double py_reward(int64_t t1, int64_t t0) {
+    return (double)or_py_micros(t1) / 1e6 - (double)or_py_micros(t0) / 1e6;
+}
+
+/* ------------------------------------------------------------------ */
+/* record / counter layouts (byte-identical to include/prisma.h)       */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    int64_t t_ns; double reward; uint32_t uid; int32_t prev;
+    uint16_t node; uint16_t dst; int8_t action; uint8_t status; uint16_t episode;
+} rec_head_t;
+
+typedef struct {
+    uint64_t events, hops, decisions, hop_deg_sum;
+    int64_t now_ns;
+    double reward_sum;
+    int32_t ov_injected, ov_arrived, ov_lost, un_injected, un_arrived, un_lost;
+    int32_t bytes_data, bytes_signaling;
+    float cost_sum, e2e_sum;
+    int32_t cost_n, e2e_n;
+    uint32_t episode, ping_rounds, seq, uid, dec_count, ctrl_dropped, error, episode_over;
+    uint64_t hops_total, events_total;
+} counters_t;
+
+enum { ST_PENDING = 0, ST_ENQUEUED = 1, ST_DROPPED = 2, ST_DEST = 3, ST_DISCARDED = 4 };
+enum { DATA_PACKET = 0, PING_FORWARD_PACKET = 3, PING_BACK_PACKET = 4 };   /* enum-and-constants.h:5-11 */
+enum { EV_PING = 0, EV_START = 1, EV_SEND = 2, EV_COMPLETE = 3, EV_RECEIVE = 4 };
+
+/* ------------------------------------------------------------------ */
+/* simulation objects                                                  */
+/* ------------------------------------------------------------------ */
+typedef struct {              /* MyTag (my-tag.h:49-65) + size */
+    int type, src, dst, next_hop, last_hop;
+    uint64_t start_time;      /* data: whole seconds; ping: ms          */
+    int valable;
+    uint32_t uid, ping_idx;
+    int tunnel;
+    float one_hop_delay;
+    uint32_t size;            /* bytes incl. PPP header                 */
+    int next_free;
+} pkt_t;
+
+typedef struct { int64_t t; uint64_t seq; int kind, id, pkt; } ev_t;
+
+typedef struct {              /* PointToPointNetDevice + DropTailQueue   */
+    int busy;
+    int *q; int q_cap, q_head, q_len;
+    uint32_t nbytes;
+    uint64_t bps;
+    int64_t delay;
+    uint32_t max_bytes;       /* byte mode if > 0                       */
+    uint32_t max_pkts;        /* packet mode otherwise                  */
+    int from_node, to_node, is_access;
+} netdev_t;
+
+typedef struct { uint32_t idx; uint64_t ms; } sent_t;
+typedef struct { sent_t* a; int n, cap; } sentvec_t;
+typedef struct { float* a; int n, cap; } fvec_t;
+typedef struct { uint32_t* a; int n, cap; } uvec_t;
+
+typedef struct {              /* temp_obs entry (forwarder.py:153-159) */
+    int64_t dec; int64_t t_ns; int active;
+} temp_t;
+
+struct or_sim {
+    or_config_t c;
+    int N, E, F, W;
+    int64_t t_end, ping_period, now;
+    uint64_t seq;
+    /* heap */
+    ev_t* heap; int hn, hcap;
+    /* packets */
+    pkt_t* pk; int pk_cap, pk_free;
+    netdev_t* dev;                 /* E switch devices + N access devices   */
+    int* flow_draws;
+    double* flow_mean;
+    uint32_t* ping_index;       /* per node m_pingPacketIndex            */
+    sentvec_t* unacked;         /* per directed link (node, tunnel)      */
+    fvec_t* delays;
+    uvec_t* lost;               /* per node m_lostPackets (uids)         */
+    temp_t* temp; int64_t temp_cap;
+    uint32_t next_uid;
+    counters_t cnt;
+    /* records */
+    unsigned char* rec; int64_t rec_n, rec_cap; int rec_bytes;
+    /* pending decision */
+    int pend; int pend_pkt, pend_node, pend_link; int64_t pend_rec;
+    int over;
+    /* trace */
+    int trace_on; int64_t* tr; int64_t tr_n, tr_cap;
+    /* last info string */
+    char info[4096];
+};
+
+static void* xrealloc(void* p, size_t n) {
+    void* q = realloc(p, n);
+    if (!q && n) { fprintf(stderr, "oracle: out of memory\n"); abort(); }
+    return q;
+}
+
+static int ev_less(const ev_t* a, const ev_t* b) {
+    return a->t < b->t || (a->t == b->t && a->seq < b->seq);
+}
+
+static void schedule(or_sim_t* s, int64_t t, int kind, int id, int pkt) {
+    if (s->hn == s->hcap) { s->hcap = s->hcap ? 2 * s->hcap : 256; s->heap = xrealloc(s->heap, sizeof(ev_t) * s->hcap); }
+    ev_t e = { t, s->seq++, kind, id, pkt };
+    int i = s->hn++;
+    while (i > 0) {
+        int p = (i - 1) / 2;
+        if (!ev_less(&e, &s->heap[p])) break;
+        s->heap[i] = s->heap[p];
+        i = p;
+    }
+    s->heap[i] = e;
+}
+
+static ev_t heap_pop(or_sim_t* s) {
+    ev_t top = s->heap[0];
+    ev_t last = s->heap[--s->hn];
+    int i = 0;
+    for (;;) {
+        int l = 2 * i + 1, r = l + 1, m = i;
+        const ev_t* mv = &last;
+        if (l < s->hn && ev_less(&s->heap[l], mv)) { m = l; mv = &s->heap[l]; }
+        if (r < s->hn && ev_less(&s->heap[r], mv)) { m = r; mv = &s->heap[r]; }
+        if (m == i) break;
+        s->heap[i] = s->heap[m];
+        i = m;
+    }
+    if (s->hn > 0) s->heap[i] = last;
+    return top;
+}
+
+static int pkt_alloc(or_sim_t* s) {
+    if (s->pk_free < 0) {
+        int old = s->pk_cap;
+        s->pk_cap = old ? old * 2 : 1024;
+        s->pk = xrealloc(s->pk, sizeof(pkt_t) * s->pk_cap);
+        for (int i = old; i < s->pk_cap; ++i) s->pk[i].next_free = (i + 1 < s->pk_cap) ? i + 1 : -1;
+        s->pk_free = old;
+    }
+    int i = s->pk_free;
+    s->pk_free = s->pk[i].next_free;
+    memset(&s->pk[i], 0, sizeof(pkt_t));
+    s->pk[i].next_free = -2;
+    return i;
+}
+
+static void pkt_free(or_sim_t* s, int i) { s->pk[i].next_free = s->pk_free; s->pk_free = i; }
+
+static void q_push(netdev_t* d, int p) {
+    if (d->q_len == d->q_cap) {
+        int nc = d->q_cap ? d->q_cap * 2 : 64;
+        int* nq = xrealloc(NULL, sizeof(int) * nc);
+        for (int i = 0; i < d->q_len; ++i) nq[i] = d->q[(d->q_head + i) % d->q_cap];
+        free(d->q);
+        d->q = nq; d->q_cap = nc; d->q_head = 0;
+    }
+    d->q[(d->q_head + d->q_len) % d->q_cap] = p;
+    d->q_len++;
+}
+
+static int q_pop(netdev_t* d) {
+    int p = d->q[d->q_head];
+    d->q_head = (d->q_head + 1) % d->q_cap;
+    d->q_len--;
+    return p;
+}
+
+#define VEC_PUSH(v, x) do { if ((v)->n == (v)->cap) { (v)->cap = (v)->cap ? 2 * (v)->cap : 8; \
+    (v)->a = xrealloc((v)->a, sizeof(*(v)->a) * (v)->cap); } (v)->a[(v)->n++] = (x); } while (0)
+
+static void vec_erase(void* base, int* n, int elem, int i) {
+    unsigned char* b = (unsigned char*)base;
+    memmove(b + (size_t)i * elem, b + (size_t)(i + 1) * elem, (size_t)(*n - i - 1) * elem);
+    (*n)--;
+}
+
+static temp_t* temp_of(or_sim_t* s, uint32_t uid) {
+    if ((int64_t)uid >= s->temp_cap) {
+        int64_t nc = s->temp_cap ? s->temp_cap : 1024;
+        while (nc <= (int64_t)uid) nc *= 2;
+        s->temp = xrealloc(s->temp, sizeof(temp_t) * nc);
+        memset(s->temp + s->temp_cap, 0, sizeof(temp_t) * (nc - s->temp_cap));
+        s->temp_cap = nc;
+    }
+    return &s->temp[uid];
+}
+
+static rec_head_t* rec_at(or_sim_t* s, int64_t d) { return (rec_head_t*)(s->rec + (size_t)d * s->rec_bytes); }
+
+static int64_t rec_new(or_sim_t* s) {
+    if (s->rec_n == s->rec_cap) {
+        s->rec_cap = s->rec_cap ? 2 * s->rec_cap : 4096;
+        s->rec = xrealloc(s->rec, (size_t)s->rec_cap * s->rec_bytes);
+    }
+    int64_t d = s->rec_n++;
+    memset(s->rec + (size_t)d * s->rec_bytes, 0, s->rec_bytes);
+    return d;
+}
+
+/* ------------------------------------------------------------------ */
+/* ComputeStats (compute-stats-v2.cc:87-217) as running sums           */
+/* ------------------------------------------------------------------ */
+static void add_loss_penalty_to_cost(or_sim_t* s) {                /* :123-126 */
+    s->cnt.cost_sum += (float)s->c.loss_penalty;
+    s->cnt.cost_n++;
+}
+
+/* ------------------------------------------------------------------ */
+/* PointToPointNetDevice (point-to-point-net-device.cc)                 */
+/* ------------------------------------------------------------------ */
+static int64_t tx_time(const netdev_t* d, uint32_t bytes) {           /* :289 */
+    return or_seconds_to_ns((double)bytes * 8 / (double)d->bps);
+}
+
+static void transmit_start(or_sim_t* s, int di, int p) {            /* :273-302 */
+    netdev_t* d = &s->dev[di];
+    d->busy = 1;
+    int64_t tx = tx_time(d, s->pk[p].size);
+    schedule(s, s->now + tx, EV_COMPLETE, di, -1);                   /* :295 */
+    schedule(s, s->now + tx + d->delay, EV_RECEIVE, di, p);           /* :296 (channel) */
+}
+
+static void transmit_complete(or_sim_t* s, int di) {                /* :305-336 */
+    netdev_t* d = &s->dev[di];
+    d->busy = 0;
+    if (d->q_len == 0) return;
+    int p = q_pop(d);
+    d->nbytes -= s->pk[p].size;
+    transmit_start(s, di, p);
+}
+
+/* DataPacketManager::dropPacket (data-packet-manager.cc:88-98), connected
+ * to MacTxDrop of every switch-switch device (:100-106). */
+static void mac_tx_drop(or_sim_t* s, int di, int p) {
+    if (s->dev[di].is_access) return;
+    const pkt_t* k = &s->pk[p];
+    for (int w = 0; w < s->N; ++w) {
+        if (k->type == DATA_PACKET && k->valable && k->dst != w && k->last_hop == w) {
+            VEC_PUSH(&s->lost[w], k->uid);
+            /* forwarder.py:214-244: loss transition of the dropping node */
+            temp_t* tp = temp_of(s, k->uid);
+            if (tp->active) {
+                rec_at(s, tp->dec)->status = ST_DROPPED;
+                s->cnt.reward_sum += s->c.loss_penalty;
+                tp->active = 0;
+            }
+        }
+    }
+}
+
+static int dev_send(or_sim_t* s, int di, int p) {                   /* :595-666 */
+    netdev_t* d = &s->dev[di];
+    pkt_t* k = &s->pk[p];
+    int ok;
+    if (d->max_bytes > 0) ok = (d->nbytes + k->size <= d->max_bytes);
+    else ok = ((uint32_t)d->q_len + 1 <= d->max_pkts);
+    if (ok) {
+        q_push(d, p);
+        d->nbytes += k->size;
+        if (!d->busy) {                                              /* :643-650 */
+            int h = q_pop(d);
+            d->nbytes -= s->pk[h].size;
+            transmit_start(s, di, h);
+        }
+        return 1;
+    }
+    if (k->type == DATA_PACKET) {                                    /* :655-664 */
+        if (k->valable && k->dst != d->from_node) {
+            s->cnt.ov_lost++;
+            add_loss_penalty_to_cost(s);
+        } else {
+            s->cnt.un_lost++;
+        }
+        mac_tx_drop(s, di, p);
+    } else {
+        s->cnt.ctrl_dropped++;
+    }
+    pkt_free(s, p);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* DataPacketManager::getObservation (data-packet-manager.cc:171-206)  */
+/* ------------------------------------------------------------------ */
+static uint32_t ping_obs_value(or_sim_t* s, int l) {
+    const fvec_t* dv = &s->delays[l];
+    double avg = 0.0;                                                /* :55-65 */
+    if (dv->n > 0) {
+        double sum = 0.0;
+        for (int i = 0; i < dv->n; ++i) sum += (double)dv->a[i];
+        avg = sum / (double)dv->n;
+    }
+    float mt = 0.0f;                                                 /* ping-back-packet-manager.cc:110-116 */
+    const sentvec_t* uv = &s->unacked[l];
+    if (uv->n > 0) {
+        double a = get_seconds(s->now) - (double)uv->a[0].ms * 0.001;
+        double b = 2.60;
+        mt = (float)((b < a) ? b : a);
+    }
+    double m = ((avg < (double)mt) ? (double)mt : avg);
+    return (uint32_t)(1000 * m);
+}
+
+static void observation(or_sim_t* s, int v, int dst, uint32_t* obs) {
+    for (int i = 0; i < s->W; ++i) obs[i] = 0;
+    obs[0] = (uint32_t)dst;                          /* identity map_overlay */
+    for (int k = s->c.row_ptr[v]; k < s->c.row_ptr[v + 1]; ++k) {
+        uint32_t val = s->c.ping_as_obs ? ping_obs_value(s, k) : s->dev[k].nbytes;
+        obs[1 + k - s->c.row_ptr[v]] = val;
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* info string (packet-manager.cc:119-176, data-packet-manager.cc:230-248) */
+/* ------------------------------------------------------------------ */
+static void build_info(or_sim_t* s, const pkt_t* k, int v) {
+    char* b = s->info;
+    size_t cap = sizeof(s->info), n = 0;
+    double now = get_seconds(s->now);
+    float avg_e2e = s->cnt.e2e_n ? s->cnt.e2e_sum / (float)s->cnt.e2e_n : 0.0f;
+    float avg_cost = s->cnt.cost_n ? s->cnt.cost_sum / (float)s->cnt.cost_n : 0.0f;
+    float sig = s->cnt.bytes_data ? (float)s->cnt.bytes_signaling / (float)s->cnt.bytes_data : 0.0f;
+    n += snprintf(b + n, cap - n, "End to End Delay=%f, Packet Size=%u, Current sim time =%f, Pkt ID =%u, packetType =%d",
+                  now - (double)k->start_time, k->size, now, k->uid, k->type);
+    n += snprintf(b + n, cap - n, ", Avg End to End Delay =%f, Avg Cost =%f, Avg Underlay End to End Delay =%f, Avg Underlay Cost =%f",
+                  (double)avg_e2e, (double)avg_cost, 0.0, 0.0);
+    n += snprintf(b + n, cap - n, ", Packets dropped =%d, Packets delivered =%d, Packets injected =%d,Packets Buffered =%d",
+                  s->cnt.ov_lost, s->cnt.ov_arrived, s->cnt.ov_injected,
+                  s->cnt.ov_injected - (s->cnt.ov_arrived + s->cnt.ov_lost));
+    n += snprintf(b + n, cap - n, ", Packets dropped Underlay =%d, Packets delivered Underlay=%d, Packets injected Underlay=%d,Packets Buffered Underlay=%d",
+                  s->cnt.un_lost, s->cnt.un_arrived, s->cnt.un_injected,
+                  s->cnt.un_injected - (s->cnt.un_arrived + s->cnt.un_lost));
+    n += snprintf(b + n, cap - n, ",Signaling overhead =%f, Packet Lost=", (double)sig);
+    uvec_t* lv = &s->lost[v];
+    while (lv->n > 0 && n < cap - 16) {
+        n += snprintf(b + n, cap - n, "%u;", lv->a[lv->n - 1]);
+        lv->n--;
+    }
+    snprintf(b + n, cap - n, ", Source=%d, Destination=%d, node=%d", k->src, k->dst, v);
+}
+
+/* ------------------------------------------------------------------ */
+/* event handlers                                                      */
+/* ------------------------------------------------------------------ */
+static void send_ping_packets(or_sim_t* s, int u) {                 /* data-packet-manager.cc:350-357 */
+    uint32_t idx = s->ping_index[u];
+    uint64_t ms = (uint64_t)(s->now / 1000000);                       /* GetMilliSeconds */
+    for (int l = s->c.row_ptr[u]; l < s->c.row_ptr[u + 1]; ++l) {     /* addSentPingForwardPacket */
+        sent_t e = { idx, ms };
+        VEC_PUSH(&s->unacked[l], e);
+    }
+    for (int l = s->c.row_ptr[u]; l < s->c.row_ptr[u + 1]; ++l) {     /* sendPingForwardPacket :360-413 */
+        int p = pkt_alloc(s);
+        pkt_t* k = &s->pk[p];
+        k->type = PING_FORWARD_PACKET;
+        k->dst = k->next_hop = s->c.link_dst[l];
+        k->last_hop = k->src = u;
+        k->start_time = ms;
+        k->tunnel = l - s->c.row_ptr[u];
+        k->ping_idx = idx;
+        k->size = 8 + 8 + 20 + 2;
+        dev_send(s, l, p);
+    }
+    s->ping_index[u] = idx + 1;
+    if (u == 0) s->cnt.ping_rounds++;
+    schedule(s, s->now + s->ping_period, EV_PING, u, -1);
+}
+
+static void ping_forward_receive(or_sim_t* s, int l_in, int p) {    /* ping-forward-packet-manager.cc:94-156 */
+    const pkt_t* k = &s->pk[p];
+    int v = s->c.link_dst[l_in];
+    float delay = (float)(get_seconds(s->now) - ((double)k->start_time * 0.001));
+    int q = pkt_alloc(s);
+    pkt_t* b = &s->pk[q];
+    k = &s->pk[p];
+    b->type = PING_BACK_PACKET;
+    b->dst = b->next_hop = k->last_hop;
+    b->last_hop = b->src = v;
+    b->one_hop_delay = delay;
+    b->ping_idx = k->ping_idx;
+    b->tunnel = k->tunnel;
+    b->size = 8 + 8 + 20 + 2;
+    dev_send(s, s->c.link_rev[l_in], q);          /* m_receivingNetDev->Send */
+}
+
+static void ping_back_receive(or_sim_t* s, int l_in, int p) {       /* ping-back-packet-manager.cc:120-144 */
+    const pkt_t* k = &s->pk[p];
+    int u = s->c.link_dst[l_in];
+    int l = s->c.row_ptr[u] + k->tunnel;
+    sentvec_t* uv = &s->unacked[l];
+    for (int i = 0; i < uv->n; ++i) {
+        if (uv->a[i].idx == k->ping_idx) { vec_erase(uv->a, &uv->n, sizeof(sent_t), i); break; }
+    }
+    fvec_t* dv = &s->delays[l];
+    if ((uint32_t)dv->n >= s->c.ma_size) vec_erase(dv->a, &dv->n, sizeof(float), 0);
+    VEC_PUSH(dv, k->one_hop_delay);
+}
+
+static void flow_schedule_next(or_sim_t* s, int f) {                /* poisson-application.cc:265-295 */
+    uint32_t key[2] = { (uint32_t)s->c.seed, s->c.replica };
+    uint32_t ctr[4] = { (uint32_t)f, (uint32_t)s->flow_draws[f], s->c.episode, 1u };
+    uint32_t x[4];
+    or_philox4x32_10(ctr, key, x);
+    uint64_t u53 = ((uint64_t)(x[0] >> 5) << 26) | (uint64_t)(x[1] >> 6);
+    double U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
+    double delay = -s->flow_mean[f] * or_det_log(U);
+    s->flow_draws[f]++;
+    schedule(s, s->now + or_seconds_to_ns(delay), EV_SEND, f, -1);
+}
+
+static void flow_send_packet(or_sim_t* s, int f) {                  /* poisson-application.cc:297-358 */
+    int p = pkt_alloc(s);
+    pkt_t* k = &s->pk[p];
+    k->type = DATA_PACKET;
+    k->dst = s->c.flow_dst[f];
+    k->src = k->next_hop = s->c.flow_src[f];
+    k->last_hop = 1000;
+    k->start_time = (uint64_t)get_seconds(s->now);                    /* :310 */
+    k->valable = 1;                                                   /* overlay pair: p = 1.0 */
+    k->uid = s->next_uid++;
+    k->size = s->c.packet_size + 8 + 20 + 2;
+    dev_send(s, s->E + s->c.flow_src[f], p);                          /* UDP socket -> access link */
+    flow_schedule_next(s, f);
+}
+
+/* Receive tail after the MacRx trace (point-to-point-net-device.cc:430-463) */
+static void receive_counters(or_sim_t* s, const pkt_t* k, int v) {
+    if (k->type == DATA_PACKET && k->dst == v) {
+        if (k->valable) {
+            if (k->next_hop == k->dst) {
+                s->cnt.ov_arrived++;
+                float x = (float)(get_seconds(s->now) - (double)k->start_time);
+                s->cnt.cost_sum += x; s->cnt.cost_n++;
+                s->cnt.e2e_sum += x; s->cnt.e2e_n++;
+            }
+        } else {
+            s->cnt.un_arrived++;
+        }
+    }
+    if (k->type > 0 && k->dst == v) s->cnt.bytes_signaling += (int32_t)(k->size - 2);
+    if (k->type == DATA_PACKET && k->last_hop == 1000) {
+        if (k->valable) { s->cnt.ov_injected++; s->cnt.bytes_data += (int32_t)(k->size - 2); }
+        else s->cnt.un_injected++;
+    }
+}
+
+/* DataPacketManager::sendPacket (data-packet-manager.cc:251-299) */
+static void finish_data_decision(or_sim_t* s, int action) {
+    int p = s->pend_pkt, v = s->pend_node;
+    int64_t d = s->pend_rec;
+    pkt_t orig = s->pk[p];
+    int deg = s->c.row_ptr[v + 1] - s->c.row_ptr[v];
+    rec_head_t* r = rec_at(s, d);
+    r->action = (int8_t)action;
+    if (action >= 0 && action < deg) {
+        int l = s->c.row_ptr[v] + action;
+        int q = pkt_alloc(s);
+        pkt_t* k = &s->pk[q];
+        *k = s->pk[p];
+        k->next_free = -2;
+        k->last_hop = v;
+        k->next_hop = s->c.link_dst[l];
+        k->size = s->c.packet_size + 8 + 20 + 2;
+        temp_t* tp = temp_of(s, k->uid);
+        tp->dec = d; tp->t_ns = s->now; tp->active = 1;
+        rec_at(s, d)->status = ST_ENQUEUED;
+        s->cnt.hops++;
+        s->cnt.hop_deg_sum += (uint64_t)deg;
+        dev_send(s, l, q);              /* a drop re-marks the record DROPPED */
+    } else {
+        rec_at(s, d)->status = ST_DISCARDED;
+    }
+    receive_counters(s, &orig, v);
+    pkt_free(s, p);
+    s->pend = 0;
+}
+
+/* PointToPointNetDevice::Receive -> PacketRoutingEnv::NotifyPktRcv
+ * (point-to-point-net-device.cc:371-467, packet-routing-gym.cc:231-267).
+ * Returns 1 when a data decision needs an action. */
+static int receive(or_sim_t* s, int di, int p) {
+    const netdev_t* d = &s->dev[di];
+    int v = d->to_node;
+    pkt_t* k = &s->pk[p];
+    if (k->type == DATA_PACKET) {
+        if (!(k->next_hop == v && k->valable)) {                      /* packet-manager.cc:115 */
+            receive_counters(s, k, v);
+            pkt_free(s, p);
+            return 0;
+        }
+        int64_t dn = rec_new(s);
+        rec_head_t* r = rec_at(s, dn);
+        temp_t* tp = temp_of(s, k->uid);
+        r->t_ns = s->now;
+        r->uid = k->uid;
+        r->node = (uint16_t)v;
+        r->dst = (uint16_t)k->dst;
+        r->episode = (uint16_t)s->c.episode;
+        r->action = -1;
+        if (tp->active) {                                             /* handle_transit_packet */
+            r->prev = (int32_t)tp->dec;
+            r->reward = py_reward(s->now, tp->t_ns);                  /* forwarder.py:360 */
+            s->cnt.reward_sum += r->reward;
+            tp->active = 0;
+        } else {
+            r->prev = -1;
+            r->reward = 0.0;
+        }
+        observation(s, v, k->dst, (uint32_t*)((unsigned char*)r + sizeof(rec_head_t)));
+        build_info(s, k, v);
+        s->cnt.decisions++;
+        if (k->dst == v) {                                            /* getGameOver: done */
+            r->status = ST_DEST;
+            receive_counters(s, k, v);                                /* sendPacket does nothing */
+            pkt_free(s, p);
+            return 0;
+        }
+        r->status = ST_PENDING;
+        s->pend = 1; s->pend_pkt = p; s->pend_node = v; s->pend_link = di; s->pend_rec = dn;
+        return 1;
+    }
+    if (k->type == PING_FORWARD_PACKET) ping_forward_receive(s, di, p);
+    else if (k->type == PING_BACK_PACKET) ping_back_receive(s, di, p);
+    receive_counters(s, &s->pk[p], v);
+    pkt_free(s, p);
+    return 0;
+}
+
+/* run events until a decision is pending (1) or the episode is over (0) */
+static int run_until_decision(or_sim_t* s) {
+    while (!s->over) {
+        if (s->hn == 0 || s->heap[0].t >= s->t_end) { s->over = 1; break; }
+        ev_t e = heap_pop(s);
+        s->now = e.t;
+        s->cnt.events++;
+        if (s->trace_on) {
+            if (s->tr_n + 4 > s->tr_cap) { s->tr_cap = s->tr_cap ? 2 * s->tr_cap : 4096; s->tr = xrealloc(s->tr, sizeof(int64_t) * s->tr_cap); }
+            s->tr[s->tr_n++] = e.t; s->tr[s->tr_n++] = (int64_t)e.seq; s->tr[s->tr_n++] = e.kind; s->tr[s->tr_n++] = e.id;
+        }
+        switch (e.kind) {
+        case EV_PING: send_ping_packets(s, e.id); break;
+        case EV_START: flow_schedule_next(s, e.id); break;             /* StartSending -> ScheduleNextTx */
+        case EV_SEND: flow_send_packet(s, e.id); break;
+        case EV_COMPLETE: transmit_complete(s, e.id); break;
+        case EV_RECEIVE:
+            if (receive(s, e.id, e.pkt)) return 1;
+            break;
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------ */
+/* public API                                                          */
+/* ------------------------------------------------------------------ */
+or_sim_t* or_create(const or_config_t* cfg) {
+    or_sim_t* s = calloc(1, sizeof(or_sim_t));
+    s->c = *cfg;
+    s->N = cfg->n_nodes; s->E = cfg->n_links; s->F = cfg->n_flows;
+    int w = 1 + cfg->max_deg; s->W = w + (w & 1);
+    s->rec_bytes = (int)sizeof(rec_head_t) + 4 * s->W;
+    s->t_end = or_seconds_to_ns(cfg->sim_time_s);
+    s->ping_period = or_seconds_to_ns((double)cfg->ping_interval_s);
+    s->pk_free = -1;
+    s->dev = calloc((size_t)(s->E + s->N), sizeof(netdev_t));
+    for (int l = 0; l < s->E; ++l) {                                  /* sim.cc:414-433 */
+        netdev_t* d = &s->dev[l];
+        d->bps = cfg->link_bps; d->delay = cfg->link_delay_ns; d->max_bytes = cfg->max_buffer_bytes;
+        d->to_node = cfg->link_dst[l]; d->is_access = 0;
+    }
+    for (int u = 0; u < s->N; ++u)
+        for (int l = cfg->row_ptr[u]; l < cfg->row_ptr[u + 1]; ++l) s->dev[l].from_node = u;
+    for (int u = 0; u < s->N; ++u) {                                  /* sim.cc:398-410 */
+        netdev_t* d = &s->dev[s->E + u];
+        int deg = cfg->row_ptr[u + 1] - cfg->row_ptr[u];
+        d->bps = (uint64_t)1000000 * cfg->link_bps * (uint64_t)deg;
+        d->delay = 0; d->max_bytes = 0; d->max_pkts = 1000;
+        d->from_node = -1; d->to_node = u; d->is_access = 1;
+    }
+    s->flow_draws = calloc((size_t)s->F + 1, sizeof(int));
+    s->flow_mean = calloc((size_t)s->F + 1, sizeof(double));
+    for (int f = 0; f < s->F; ++f)
+        s->flow_mean[f] = (double)(cfg->packet_size * 8u) / (double)cfg->flow_rate_bps[f];
+    s->ping_index = calloc((size_t)s->N, sizeof(uint32_t));
+    s->unacked = calloc((size_t)s->E + 1, sizeof(sentvec_t));
+    s->delays = calloc((size_t)s->E + 1, sizeof(fvec_t));
+    s->lost = calloc((size_t)s->N, sizeof(uvec_t));
+    s->cnt.episode = cfg->episode;
+    /* setup-time schedule: ping timers (sim.cc:544 -> data-packet-manager.cc:118-121)
+       in overlay order, then application starts (Node::Initialize at t=0) in
+       flow (src, dst) order (sim.cc:599-631) */
+    for (int u = 0; u < s->N; ++u) schedule(s, s->ping_period, EV_PING, u, -1);
+    uint32_t key[2] = { (uint32_t)cfg->seed, cfg->replica };
+    for (int f = 0; f < s->F; ++f) {
+        uint32_t ctr[4] = { (uint32_t)f, 0u, cfg->episode, 0u };
+        uint32_t x[4];
+        or_philox4x32_10(ctr, key, x);
+        uint64_t u53 = ((uint64_t)(x[0] >> 5) << 26) | (uint64_t)(x[1] >> 6);
+        double U = (double)u53 * (1.0 / 9007199254740992.0);
+        schedule(s, or_seconds_to_ns(0.0001 + U), EV_START, f, -1);
+    }
+    return s;
+}
+
+void or_destroy(or_sim_t* s) {
+    if (!s) return;
+    for (int i = 0; i < s->E + s->N; ++i) free(s->dev[i].q);
+    for (int l = 0; l < s->E; ++l) { free(s->unacked[l].a); free(s->delays[l].a); }
+    for (int u = 0; u < s->N; ++u) free(s->lost[u].a);
+    free(s->dev); free(s->flow_draws); free(s->flow_mean); free(s->ping_index);
+    free(s->unacked); free(s->delays); free(s->lost); free(s->temp);
+    free(s->heap); free(s->pk); free(s->rec); free(s->tr);
+    free(s);
+}
+
+int or_step(or_sim_t* s, int32_t action, int32_t* obs_out) {
+    if (s->pend) finish_data_decision(s, action);
+    int r = run_until_decision(s);
+    if (r && obs_out) {
+        const uint32_t* o = (const uint32_t*)((unsigned char*)rec_at(s, s->pend_rec) + sizeof(rec_head_t));
+        for (int i = 0; i < s->W; ++i) obs_out[i] = (int32_t)o[i];
+    }
+    return r;
+}
+
+int64_t or_run_table(or_sim_t* s, const uint8_t* table, int64_t max_hops) {
+    uint64_t h0 = s->cnt.hops;
+    while ((int64_t)(s->cnt.hops - h0) < max_hops) {
+        if (s->pend) {
+            rec_head_t* r = rec_at(s, s->pend_rec);
+            finish_data_decision(s, table[(size_t)r->node * s->N + r->dst]);
+            continue;
+        }
+        if (!run_until_decision(s)) break;
+    }
+    return (int64_t)(s->cnt.hops - h0);
+}
+
+int64_t or_record_count(const or_sim_t* s) { return s->rec_n; }
+int32_t or_obs_width(const or_sim_t* s) { return s->W; }
+
+int64_t or_copy_records(const or_sim_t* s, int64_t first, int64_t count, void* out) {
+    if (first < 0 || first > s->rec_n) return 0;
+    if (first + count > s->rec_n) count = s->rec_n - first;
+    memcpy(out, s->rec + (size_t)first * s->rec_bytes, (size_t)count * s->rec_bytes);
+    return count;
+}
+
+void or_counters(const or_sim_t* s, void* out) {
+    counters_t c = s->cnt;
+    c.now_ns = s->now;
+    c.seq = (uint32_t)s->seq;
+    c.uid = s->next_uid;
+    c.dec_count = (uint32_t)s->rec_n;
+    c.episode_over = (uint32_t)s->over;
+    c.hops_total = c.hops;
+    c.events_total = c.events;
+    memcpy(out, &c, sizeof(c));
+}
+
+void or_enable_trace(or_sim_t* s, int on) { s->trace_on = on; }
+int64_t or_trace_count(const or_sim_t* s) { return s->tr_n / 4; }
+int64_t or_copy_trace(const or_sim_t* s, int64_t first, int64_t count, int64_t* out4) {
+    int64_t n = s->tr_n / 4;
+    if (first < 0 || first > n) return 0;
+    if (first + count > n) count = n - first;
+    memcpy(out4, s->tr + first * 4, (size_t)count * 4 * sizeof(int64_t));
+    return count;
+}
+
+int32_t or_last_info(const or_sim_t* s, char* buf, int32_t cap) {
+    int32_t n = (int32_t)strlen(s->info);
+    if (cap <= 0) return n;
+    int32_t m = n < cap - 1 ? n : cap - 1;
+    memcpy(buf, s->info, (size_t)m);
+    buf[m] = 0;
+    return m;
+}

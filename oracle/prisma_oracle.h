@@ -1,0 +1,90 @@
+/*
+ * prisma_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's ns-3 packet-hop semantics, used as the
+ * parity checker for the HIP engine (tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg only; never linked into the product).
+ *
+ * The ns-3 C++ path of the reference cannot be built here (ns-3/ns3-gym,
+ * waf, libzmq and protobuf are absent), so this is a literal
+ * single-replica discrete-event restatement: a binary min-heap of
+ * (time_ns, uid) events — ns-3's MapScheduler order — with one handler per
+ * ns-3 callback, written independently of the GPU engine (own data
+ * structures, own RNG code).  Parity is "GPU == oracle" bit-exact; parity of
+ * the oracle with real ns-3 RNG draws is unpinned and is
+ * pinned instead by analytic known answers and networkx fixtures.
+ */
+#ifndef PRISMA_ORACLE_H
+#define PRISMA_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_config {
+    int32_t n_nodes, n_links, n_flows, max_deg;
+    const int32_t*  row_ptr;
+    const int32_t*  link_dst;
+    const int32_t*  link_rev;
+    const int32_t*  flow_src;
+    const int32_t*  flow_dst;
+    const uint64_t* flow_rate_bps;
+    uint64_t link_bps;
+    int64_t  link_delay_ns;
+    uint32_t max_buffer_bytes;
+    uint32_t packet_size;
+    double   sim_time_s;
+    float    ping_interval_s;
+    uint32_t ma_size;
+    uint32_t ping_as_obs;
+    uint32_t auto_reset;        /* ignored by the oracle (single episode) */
+    double   loss_penalty;
+    uint64_t seed;
+    uint32_t replica;           /* global replica id (Philox key word 1)   */
+    uint32_t episode;
+} or_config_t;
+
+typedef struct or_sim or_sim_t;
+
+or_sim_t* or_create(const or_config_t* cfg);
+void      or_destroy(or_sim_t* s);
+
+/* Apply `action` to the pending decision (ignored if none is pending), then
+ * run until the next decision that needs an action.  Returns 1 if a
+ * decision is pending (obs written to obs_out[obs_width]), 0 if the episode
+ * is over. */
+int or_step(or_sim_t* s, int32_t action, int32_t* obs_out);
+
+/* Run with a [N][N] action table until `max_hops` more hops were executed
+ * or the episode ended.  Returns hops executed. */
+int64_t or_run_table(or_sim_t* s, const uint8_t* table, int64_t max_hops);
+
+/* Records (same byte layout as prisma_record_t; 32 + 4*obs_width bytes). */
+int64_t or_record_count(const or_sim_t* s);
+int32_t or_obs_width(const or_sim_t* s);
+int64_t or_copy_records(const or_sim_t* s, int64_t first, int64_t count, void* out);
+
+/* Counters with the same byte layout as prisma_counters_t. */
+void or_counters(const or_sim_t* s, void* out);
+
+/* Optional event trace: (t_ns, seq, kind, id) per executed event. */
+void    or_enable_trace(or_sim_t* s, int on);
+int64_t or_trace_count(const or_sim_t* s);
+int64_t or_copy_trace(const or_sim_t* s, int64_t first, int64_t count, int64_t* out4);
+
+/* The decision "info" string of the reference (packet-manager.cc:119-176 +
+ * data-packet-manager.cc:230-248) for the last decision, as the compat shim
+ * needs it.  Returns bytes written (excluding NUL). */
+int32_t or_last_info(const or_sim_t* s, char* buf, int32_t cap);
+
+/* Exposed building blocks for known-answer tests. */
+void     or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+double   or_det_log(double x);
+int64_t  or_seconds_to_ns(double s);
+uint64_t or_py_micros(int64_t t_ns);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,92 @@
+// engine_layout.h — per-replica state image shared by host sizing code and
+// the gfx950 kernels.  The same byte image lives in HBM between launches
+// and in LDS while a wavefront advances its replica.
+#pragma once
+#include <stdint.h>
+
+namespace prisma {
+
+constexpr int kWave = 64;
+
+// event kinds in the candidate code (kind << 28 | index)
+constexpr uint32_t K_PING = 0u, K_FLOW = 1u, K_COMPLETE = 2u, K_ARRIVE = 3u;
+
+// packet types (enum-and-constants.h:5-11)
+constexpr uint32_t T_DATA = 0u, T_PING_FWD = 3u, T_PING_BACK = 4u;
+
+// packet entry (16 bytes) fields, word x:
+//   bits 0-2 type | 3-10 src | 11-18 dst | 19 fresh (lastHop==1000) |
+//   20 valable | 21-31: data -> start second (11 bits), ping -> tunnel (8 bits)
+// y: data uid, ping index;  z: data prev decision, ping-fwd start_ms,
+// ping-back one-hop delay (f32 bits);  w: data decision time in us.
+__host__ __device__ inline uint32_t ent_type(uint32_t x) { return x & 7u; }
+__host__ __device__ inline uint32_t ent_src(uint32_t x) { return (x >> 3) & 255u; }
+__host__ __device__ inline uint32_t ent_dst(uint32_t x) { return (x >> 11) & 255u; }
+__host__ __device__ inline uint32_t ent_fresh(uint32_t x) { return (x >> 19) & 1u; }
+__host__ __device__ inline uint32_t ent_aux(uint32_t x) { return x >> 21; }
+__host__ __device__ inline uint32_t ent_make(uint32_t type, uint32_t src, uint32_t dst, uint32_t fresh,
+                                             uint32_t valable, uint32_t aux) {
+    return type | (src << 3) | (dst << 11) | (fresh << 19) | (valable << 20) | (aux << 21);
+}
+
+struct Hdr {                 // 128 bytes at state offset 0
+    int64_t  now;
+    int64_t  ping_t;
+    uint32_t ping_seq;
+    uint32_t seq;
+    uint32_t uid;
+    uint32_t dec_count;
+    uint32_t pend;           // 1: a decision waits for an action
+    uint32_t pend_link;
+    uint32_t pend_node;
+    uint32_t pend_dec;
+    uint32_t pend_ent[4];
+    uint32_t ping_rounds;
+    uint32_t episode;
+    uint32_t over;
+    uint32_t error;
+    uint32_t stop;
+    uint32_t hops_launch;
+    uint64_t hops_total;
+    uint64_t events_total;
+    uint32_t pad[6];
+};
+static_assert(sizeof(Hdr) == 128, "Hdr size");
+
+struct LinkState {           // 32 bytes
+    int64_t  complete_t;
+    uint32_t complete_seq;
+    uint32_t q_bytes;        // bytes waiting in the FIFO (excl. the wire)
+    uint16_t head, txp, tail, n_wire;
+    uint16_t n_queue, busy, pad0, pad1;
+};
+static_assert(sizeof(LinkState) == 32, "LinkState size");
+
+struct PingMeta {            // 16 bytes per directed link (= tunnel of its source)
+    int32_t  acked_last;     // highest ping index acknowledged, -1 none
+    int32_t  first_hole;     // lowest never-acknowledged index below acked_last, -1 none
+    uint32_t win_n;
+    uint32_t win_head;
+};
+
+// Offsets (bytes) of every region; filled on the host, passed by value.
+struct Layout {
+    int32_t N, E, L, F, W, max_deg, WCAP, MA;
+    uint32_t topo_bytes, state_bytes, lds_bytes, table_bytes;
+    // topology image (LDS offset 0)
+    uint32_t t_rowptr, t_ldst, t_lrev, t_lfrom, t_txd, t_txp, t_prop, t_rofs, t_rcap, t_qmax,
+             t_fsrc, t_fdst, t_fmean, t_table;
+    // state image (LDS offset topo_bytes)
+    uint32_t s_hdr, s_cnt, s_obs, s_ft, s_fseq, s_fdraw, s_link, s_wt, s_wseq, s_ring, s_win, s_pmeta;
+    // scenario constants
+    int64_t  t_end, ping_period;
+    uint32_t data_size, ping_size;
+    uint32_t ma, ping_as_obs, auto_reset;
+    uint32_t seed_lo, replica_base;
+    uint32_t log_cap, rec_bytes;
+    double   loss_penalty;
+    float    loss_penalty_f;
+    uint32_t pad;
+};
+
+}  // namespace prisma

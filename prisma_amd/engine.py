@@ -1,0 +1,213 @@
+"""ctypes binding of libprisma_amd.so (include/prisma.h) on torch HIP memory.
+
+The library is the product: every simulation step runs in its gfx950
+kernels.  There is no CPU fallback — if the shared library is missing or no
+gfx950 device is present, construction raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional
+
+import numpy as np
+
+from .records import COUNTERS_DTYPE, record_dtype
+from .topology import Topology
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprisma_amd.so")
+
+PRISMA_POLICY_TABLE = 1
+
+
+class PrismaError(RuntimeError):
+    pass
+
+
+class _Topo(C.Structure):
+    _fields_ = [
+        ("n_nodes", C.c_int32), ("n_links", C.c_int32), ("n_flows", C.c_int32), ("max_deg", C.c_int32),
+        ("row_ptr", C.c_void_p), ("link_dst", C.c_void_p), ("link_rev", C.c_void_p),
+        ("flow_src", C.c_void_p), ("flow_dst", C.c_void_p), ("flow_rate_bps", C.c_void_p),
+    ]
+
+
+class _Params(C.Structure):
+    _fields_ = [
+        ("link_bps", C.c_uint64), ("link_delay_ns", C.c_int64), ("max_buffer_bytes", C.c_uint32),
+        ("packet_size", C.c_uint32), ("sim_time_s", C.c_double), ("ping_interval_s", C.c_float),
+        ("ma_size", C.c_uint32), ("ping_as_obs", C.c_uint32), ("auto_reset", C.c_uint32),
+        ("loss_penalty", C.c_double), ("seed", C.c_uint64), ("replica_base", C.c_uint32),
+        ("log_capacity", C.c_uint32),
+    ]
+
+
+class _LogView(C.Structure):
+    _fields_ = [("records", C.c_void_p), ("record_bytes", C.c_uint32), ("log_capacity", C.c_uint32),
+                ("obs_width", C.c_int32), ("n_replicas", C.c_int32)]
+
+
+EXPORTS = [
+    "prisma_abi_version", "prisma_last_error", "prisma_create", "prisma_reset", "prisma_step", "prisma_run",
+    "prisma_read_counters", "prisma_counters_device", "prisma_log_view", "prisma_copy_log",
+    "prisma_state_bytes", "prisma_destroy",
+]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libprisma_amd.so and declare its C-ABI (raises if absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise PrismaError(f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(path)
+    L.prisma_abi_version.restype = C.c_int
+    L.prisma_last_error.restype = C.c_char_p
+    L.prisma_create.restype = C.c_int
+    L.prisma_create.argtypes = [C.POINTER(_Topo), C.POINTER(_Params), C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
+    L.prisma_reset.restype = C.c_int
+    L.prisma_reset.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+    L.prisma_step.restype = C.c_int
+    L.prisma_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.prisma_run.restype = C.c_int
+    L.prisma_run.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]
+    L.prisma_read_counters.restype = C.c_int
+    L.prisma_read_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.prisma_counters_device.restype = C.c_int
+    L.prisma_counters_device.argtypes = [C.c_void_p, C.POINTER(C.c_void_p)]
+    L.prisma_log_view.restype = C.c_int
+    L.prisma_log_view.argtypes = [C.c_void_p, C.POINTER(_LogView)]
+    L.prisma_copy_log.restype = C.c_int
+    L.prisma_copy_log.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+    L.prisma_state_bytes.restype = C.c_int
+    L.prisma_state_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    L.prisma_destroy.restype = None
+    L.prisma_destroy.argtypes = [C.c_void_p]
+    if L.prisma_abi_version() != 1:
+        raise PrismaError("libprisma_amd ABI version mismatch")
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = _lib.prisma_last_error().decode(errors="replace")
+        raise PrismaError(f"prisma error {rc}: {msg}")
+
+
+def _stream_handle(stream) -> Optional[int]:
+    if stream is None:
+        import torch
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream)
+
+
+class PrismaEngine:
+    """R replicas of one scenario on one MI355X (device memory owned by the library)."""
+
+    def __init__(self, topo: Topology, params: dict, n_replicas: int, device: int = 0):
+        import torch
+        if not torch.cuda.is_available():
+            raise PrismaError("PrismaEngine needs a HIP device (no CPU fallback)")
+        L = load_library()
+        self.topo = topo
+        self.params = dict(params)
+        self.R = int(n_replicas)
+        self.device = int(device)
+        self.torch_device = torch.device("cuda", self.device)
+        self._keep = [np.ascontiguousarray(topo.row_ptr, dtype=np.int32),
+                      np.ascontiguousarray(topo.link_dst, dtype=np.int32),
+                      np.ascontiguousarray(topo.link_rev, dtype=np.int32),
+                      np.ascontiguousarray(topo.flow_src, dtype=np.int32),
+                      np.ascontiguousarray(topo.flow_dst, dtype=np.int32),
+                      np.ascontiguousarray(topo.flow_rate_bps, dtype=np.uint64)]
+        t = _Topo(topo.n_nodes, topo.n_links, topo.n_flows, topo.max_deg,
+                  *[a.ctypes.data for a in self._keep])
+        p = _Params(**{k: params[k] for k, _ in _Params._fields_})
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            _check(L.prisma_create(C.byref(t), C.byref(p), self.R, self.device, C.byref(h)))
+        self.h = h
+        lv = _LogView()
+        _check(L.prisma_log_view(self.h, C.byref(lv)))
+        self.W = int(lv.obs_width)
+        self.rec_bytes = int(lv.record_bytes)
+        self.log_capacity = int(lv.log_capacity)
+        self.rec_dtype = record_dtype(self.W)
+        sb, lb = C.c_uint32(), C.c_uint32()
+        _check(L.prisma_state_bytes(self.h, C.byref(sb), C.byref(lb)))
+        self.state_bytes, self.lds_bytes = int(sb.value), int(lb.value)
+        self.obs = torch.zeros((self.R, self.W), dtype=torch.int32, device=self.torch_device)
+        self.mask = torch.zeros(self.R, dtype=torch.uint8, device=self.torch_device)
+
+    # -- lifecycle --------------------------------------------------------
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.prisma_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def reset(self, episode: int = 0, stream=None):
+        _check(_lib.prisma_reset(self.h, int(episode), _stream_handle(stream)))
+
+    # -- hot path ---------------------------------------------------------
+    def step(self, actions=None, stream=None):
+        """Apply actions [R] (int32 on device) to pending decisions, advance to the next ones."""
+        a = 0
+        if actions is not None:
+            if actions.dtype != self.obs.dtype or actions.numel() != self.R or not actions.is_cuda:
+                raise PrismaError("actions must be a device int32 tensor of n_replicas elements")
+            a = actions.contiguous().data_ptr()
+        _check(_lib.prisma_step(self.h, a or None, self.obs.data_ptr(), self.mask.data_ptr(), _stream_handle(stream)))
+        return self.obs, self.mask
+
+    def run(self, table, max_hops: int, stream=None):
+        """Fused policy: every replica executes up to max_hops hops with an [N, N] action table."""
+        import torch
+        n = self.topo.n_nodes
+        if table.dtype != torch.uint8 or tuple(table.shape) != (n, n) or not table.is_cuda:
+            raise PrismaError("table must be a device uint8 tensor of shape [n_nodes, n_nodes]")
+        _check(_lib.prisma_run(self.h, PRISMA_POLICY_TABLE, table.contiguous().data_ptr(), int(max_hops),
+                               _stream_handle(stream)))
+
+    # -- outputs ----------------------------------------------------------
+    def counters(self, stream=None) -> np.ndarray:
+        out = np.zeros(self.R, dtype=COUNTERS_DTYPE)
+        _check(_lib.prisma_read_counters(self.h, out.ctypes.data, _stream_handle(stream)))
+        return out
+
+    def counters_tensor(self):
+        """Device counters as a torch uint8 [R, 144] copy (for collectives)."""
+        import torch
+        ptr = C.c_void_p()
+        _check(_lib.prisma_counters_device(self.h, C.byref(ptr)))
+        host = self.counters()
+        return torch.from_numpy(host.view(np.uint8).reshape(self.R, COUNTERS_DTYPE.itemsize).copy()).to(self.torch_device)
+
+    def log_tensor(self, stream=None):
+        import torch
+        nbytes = self.R * self.log_capacity * self.rec_bytes
+        buf = torch.empty(nbytes, dtype=torch.uint8, device=self.torch_device)
+        _check(_lib.prisma_copy_log(self.h, buf.data_ptr(), nbytes, _stream_handle(stream)))
+        return buf.view(self.R, self.log_capacity, self.rec_bytes)
+
+    def records(self, replica: int, first: int, count: int, log_host: Optional[np.ndarray] = None) -> np.ndarray:
+        """Records [first, first+count) of one replica in decision order (host numpy)."""
+        if log_host is None:
+            import torch
+            torch.cuda.synchronize(self.device)
+            log_host = self.log_tensor().cpu().numpy()
+        if count > self.log_capacity:
+            raise PrismaError("requested more records than the log ring holds")
+        cap = self.log_capacity
+        idx = (np.arange(first, first + count) % cap)
+        raw = log_host[replica][idx]
+        return raw.reshape(-1).view(self.rec_dtype)
