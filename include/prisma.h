@@ -200,9 +200,10 @@ int prisma_reset(prisma_env_t* env, uint32_t episode, void* stream);
  * NULL on the first call after reset), then advance every replica to its
  * next pending decision.  obs_out: device int32 [n_replicas][obs_width];
  * mask_out: device uint8 [n_replicas] (1 = a decision is pending, 0 =
- * episode over).  Either output may be NULL. */
+ * episode over); node_out: device int32 [n_replicas], the node deciding
+ * (-1 if none).  Any output may be NULL. */
 int prisma_step(prisma_env_t* env, const int32_t* actions, int32_t* obs_out,
-                uint8_t* mask_out, void* stream);
+                uint8_t* mask_out, int32_t* node_out, void* stream);
 
 /* Fused policy: advance every replica by up to max_hops hops, deciding
  * in-kernel with `table` (device uint8 [n_nodes][n_nodes] action table). */
@@ -223,6 +224,15 @@ int prisma_log_view(prisma_env_t* env, prisma_log_view_t* out);
 /* Device-to-device copy of the whole log ring ([n_replicas][log_capacity]
  * records) into caller memory of at least `bytes` bytes, on `stream`. */
 int prisma_copy_log(prisma_env_t* env, void* dst_device, uint64_t bytes, void* stream);
+
+/* Device-to-device copy of the counters (prisma_counters_t [n_replicas]). */
+int prisma_copy_counters(prisma_env_t* env, void* dst_device, void* stream);
+
+/* Gather n decision records, record dec[i] of replica replica[i] (both
+ * device arrays), into dst_device (n * record_bytes bytes).  The caller
+ * keeps dec[i] within the last log_capacity decisions of that replica. */
+int prisma_gather_records(prisma_env_t* env, const int32_t* replica, const uint32_t* dec,
+                          int32_t n, void* dst_device, void* stream);
 
 /* Bytes of per-replica state (the LDS image) and LDS bytes per workgroup. */
 int prisma_state_bytes(prisma_env_t* env, uint32_t* state_bytes,

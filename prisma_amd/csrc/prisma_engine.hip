@@ -131,6 +131,7 @@ struct KParams {
     const int32_t* actions;      // [R] or null
     int32_t* obs_out;            // [R][W] or null
     uint8_t* mask_out;           // [R] or null
+    int32_t* node_out;           // [R] or null
     const uint8_t* table;        // [N][N] or null
     int32_t R;
     int32_t max_hops;
@@ -503,6 +504,7 @@ __device__ void init_replica(Sim& S, int lane, uint32_t episode) {
     const Layout& L = *S.L;
     uint32_t dec = S.h->dec_count;                 // monotonic across episodes
     uint64_t ht = S.h->hops_total, et = S.h->events_total;
+    uint32_t hl = S.h->hops_launch;                // per-launch budget survives resets
     __syncthreads();
     uint4* st4 = (uint4*)(S.base + L.topo_bytes);
     for (uint32_t i = (uint32_t)lane; i < L.state_bytes / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
@@ -533,6 +535,7 @@ __device__ void init_replica(Sim& S, int lane, uint32_t episode) {
         h.dec_count = dec;
         h.hops_total = ht;
         h.events_total = et;
+        h.hops_launch = hl;
         h.episode = episode;
         S.c->episode = episode;
     }
@@ -668,12 +671,14 @@ extern "C" __global__ void __launch_bounds__(64) prisma_step_kernel(KParams P) {
     }
     __syncthreads();
 
+    uint32_t resets = 0;
     while (!S.h->stop) {
         int64_t bt;
         uint32_t bs, bc;
         select_event(S, lane, bt, bs, bc);
         if (bt >= L.t_end) {                         // Simulator::Stop(simTime) (sim.cc:703)
-            if (L.auto_reset) {
+            if (L.auto_reset && resets < 64u) {   // bounded: an empty scenario cannot spin forever
+                ++resets;
                 init_replica(S, lane, S.h->episode + 1u);
                 continue;
             }
@@ -709,10 +714,28 @@ extern "C" __global__ void __launch_bounds__(64) prisma_step_kernel(KParams P) {
 
     const bool pending = S.h->pend && !S.h->over;
     if (P.mask_out && lane == 0) P.mask_out[r] = pending ? 1 : 0;
+    if (P.node_out && lane == 0) P.node_out[r] = pending ? (int32_t)S.h->pend_node : -1;
     if (P.obs_out && lane < L.W) P.obs_out[(size_t)r * L.W + lane] = pending ? (int32_t)S.obs[lane] : 0;
     publish_counters(S, P, r, lane);
     __syncthreads();
     stage_out(lds, P, r, lane);
+}
+
+// Gather records (replica[i], dec[i]) into a dense array: one lane per 4-byte
+// word, a wave per group of records (record rows are 48-64 B, so a wave
+// writes 1 KiB contiguous destination rows).
+extern "C" __global__ void __launch_bounds__(256) prisma_gather_kernel(
+        const unsigned char* log, uint32_t log_cap, uint32_t rec_bytes, const int32_t* replica,
+        const uint32_t* dec, int32_t n, uint32_t* dst) {
+    const uint32_t words = rec_bytes / 4u;
+    const uint64_t total = (uint64_t)n * words;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t k = i / words;
+        uint32_t w = (uint32_t)(i - k * words);
+        const uint32_t* src = (const uint32_t*)(log + ((size_t)replica[k] * log_cap + (dec[k] & (log_cap - 1))) * rec_bytes);
+        dst[i] = src[w];
+    }
 }
 
 // ===========================================================================
@@ -965,7 +988,8 @@ extern "C" int prisma_reset(prisma_env_t* e, uint32_t episode, void* stream) {
     return rc;
 }
 
-extern "C" int prisma_step(prisma_env_t* e, const int32_t* actions, int32_t* obs_out, uint8_t* mask_out, void* stream) {
+extern "C" int prisma_step(prisma_env_t* e, const int32_t* actions, int32_t* obs_out, uint8_t* mask_out,
+                           int32_t* node_out, void* stream) {
     if (!e) return set_err(PRISMA_ERR_ARG, "null env");
     if (!e->reset_done) return set_err(PRISMA_ERR_STATE, "prisma_reset must be called first");
     KParams P = base_params(e);
@@ -973,6 +997,7 @@ extern "C" int prisma_step(prisma_env_t* e, const int32_t* actions, int32_t* obs
     P.actions = actions;
     P.obs_out = obs_out;
     P.mask_out = mask_out;
+    P.node_out = node_out;
     P.max_hops = 0x7fffffff;
     return launch(e, (const void*)prisma_step_kernel, P, stream);
 }
@@ -1022,6 +1047,31 @@ extern "C" int prisma_copy_log(prisma_env_t* e, void* dst_device, uint64_t bytes
     (void)hipSetDevice(e->device);
     if (!HIP_OK(hipMemcpyAsync(dst_device, e->d_log, total, hipMemcpyDeviceToDevice, (hipStream_t)stream)))
         return set_err(PRISMA_ERR_DEVICE, "log copy failed");
+    return PRISMA_OK;
+}
+
+extern "C" int prisma_copy_counters(prisma_env_t* e, void* dst_device, void* stream) {
+    if (!e || !dst_device) return set_err(PRISMA_ERR_ARG, "null argument");
+    (void)hipSetDevice(e->device);
+    if (!HIP_OK(hipMemcpyAsync(dst_device, e->d_cnt, sizeof(prisma_counters_t) * e->R, hipMemcpyDeviceToDevice,
+                               (hipStream_t)stream)))
+        return set_err(PRISMA_ERR_DEVICE, "counter copy failed");
+    return PRISMA_OK;
+}
+
+extern "C" int prisma_gather_records(prisma_env_t* e, const int32_t* replica, const uint32_t* dec, int32_t n,
+                                     void* dst_device, void* stream) {
+    if (!e || (n > 0 && (!replica || !dec || !dst_device))) return set_err(PRISMA_ERR_ARG, "null argument");
+    if (n <= 0) return PRISMA_OK;
+    (void)hipSetDevice(e->device);
+    uint64_t total = (uint64_t)n * (e->lay.rec_bytes / 4u);
+    unsigned grid = (unsigned)((total + 255) / 256);
+    if (grid > 8192u) grid = 8192u;
+    hipLaunchKernelGGL(prisma_gather_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned char*)e->d_log, e->lay.log_cap, e->lay.rec_bytes, replica, dec, n,
+                       (uint32_t*)dst_device);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return set_err(PRISMA_ERR_LAUNCH, std::string("gather launch failed: ") + hipGetErrorString(err));
     return PRISMA_OK;
 }
 

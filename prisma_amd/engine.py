@@ -50,7 +50,7 @@ class _LogView(C.Structure):
 EXPORTS = [
     "prisma_abi_version", "prisma_last_error", "prisma_create", "prisma_reset", "prisma_step", "prisma_run",
     "prisma_read_counters", "prisma_counters_device", "prisma_log_view", "prisma_copy_log",
-    "prisma_state_bytes", "prisma_destroy",
+    "prisma_copy_counters", "prisma_gather_records", "prisma_state_bytes", "prisma_destroy",
 ]
 
 _lib = None
@@ -71,7 +71,7 @@ def load_library(path: str = LIB_PATH):
     L.prisma_reset.restype = C.c_int
     L.prisma_reset.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
     L.prisma_step.restype = C.c_int
-    L.prisma_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.prisma_step.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
     L.prisma_run.restype = C.c_int
     L.prisma_run.argtypes = [C.c_void_p, C.c_int32, C.c_void_p, C.c_int32, C.c_void_p]
     L.prisma_read_counters.restype = C.c_int
@@ -82,6 +82,10 @@ def load_library(path: str = LIB_PATH):
     L.prisma_log_view.argtypes = [C.c_void_p, C.POINTER(_LogView)]
     L.prisma_copy_log.restype = C.c_int
     L.prisma_copy_log.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+    L.prisma_copy_counters.restype = C.c_int
+    L.prisma_copy_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.prisma_gather_records.restype = C.c_int
+    L.prisma_gather_records.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
     L.prisma_state_bytes.restype = C.c_int
     L.prisma_state_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.prisma_destroy.restype = None
@@ -142,6 +146,7 @@ class PrismaEngine:
         self.state_bytes, self.lds_bytes = int(sb.value), int(lb.value)
         self.obs = torch.zeros((self.R, self.W), dtype=torch.int32, device=self.torch_device)
         self.mask = torch.zeros(self.R, dtype=torch.uint8, device=self.torch_device)
+        self.node = torch.zeros(self.R, dtype=torch.int32, device=self.torch_device)
 
     # -- lifecycle --------------------------------------------------------
     def close(self):
@@ -166,8 +171,9 @@ class PrismaEngine:
             if actions.dtype != self.obs.dtype or actions.numel() != self.R or not actions.is_cuda:
                 raise PrismaError("actions must be a device int32 tensor of n_replicas elements")
             a = actions.contiguous().data_ptr()
-        _check(_lib.prisma_step(self.h, a or None, self.obs.data_ptr(), self.mask.data_ptr(), _stream_handle(stream)))
-        return self.obs, self.mask
+        _check(_lib.prisma_step(self.h, a or None, self.obs.data_ptr(), self.mask.data_ptr(), self.node.data_ptr(),
+                                _stream_handle(stream)))
+        return self.obs, self.mask, self.node
 
     def run(self, table, max_hops: int, stream=None):
         """Fused policy: every replica executes up to max_hops hops with an [N, N] action table."""
@@ -184,13 +190,24 @@ class PrismaEngine:
         _check(_lib.prisma_read_counters(self.h, out.ctypes.data, _stream_handle(stream)))
         return out
 
-    def counters_tensor(self):
-        """Device counters as a torch uint8 [R, 144] copy (for collectives)."""
+    def counters_tensor(self, stream=None):
+        """Device copy of the counters as a torch uint8 tensor [R, 144] (for device-side use / collectives)."""
         import torch
-        ptr = C.c_void_p()
-        _check(_lib.prisma_counters_device(self.h, C.byref(ptr)))
-        host = self.counters()
-        return torch.from_numpy(host.view(np.uint8).reshape(self.R, COUNTERS_DTYPE.itemsize).copy()).to(self.torch_device)
+        buf = torch.empty((self.R, COUNTERS_DTYPE.itemsize), dtype=torch.uint8, device=self.torch_device)
+        _check(_lib.prisma_copy_counters(self.h, buf.data_ptr(), _stream_handle(stream)))
+        return buf
+
+    def gather_records(self, replica, dec, stream=None):
+        """Device gather of records -> torch uint8 [n, rec_bytes] (replica int32, dec int32/uint32 on device)."""
+        import torch
+        n = int(replica.numel())
+        out = torch.empty((max(n, 1), self.rec_bytes), dtype=torch.uint8, device=self.torch_device)
+        if n:
+            rep = replica.to(torch.int32).contiguous()
+            d = dec.to(torch.int32).contiguous()
+            _check(_lib.prisma_gather_records(self.h, rep.data_ptr(), d.data_ptr(), n, out.data_ptr(),
+                                              _stream_handle(stream)))
+        return out[:n]
 
     def log_tensor(self, stream=None):
         import torch

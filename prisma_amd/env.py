@@ -1,0 +1,156 @@
+"""Gym-style batched surface over the engine (the drop-in for Ns3Env at scale).
+
+The reference drives one ``ns3env.Ns3Env`` per overlay node over ZMQ
+(ns3env.py:378-455; forwarder.py:291-332): ``reset() -> obs``,
+``step(action) -> (obs, reward, done, info)`` where ``obs`` is the next data
+packet waiting at that node, ``done`` says it reached its destination and
+the Q-routing reward is recovered by the agent from time stamps in ``info``.
+
+``VecRoutingEnv`` keeps that contract for R replicas at once: every replica
+always has exactly one pending forwarding decision (at whatever node the
+next data packet arrives), ``step(actions)`` applies one action per replica
+and returns the next pending decisions.  What the reference forwarder
+reconstructs from the info string — per-hop (obs, action, reward, next_obs,
+done) transitions and the loss transitions — is produced on the device by
+``transitions()``, joined from the engine's decision log.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .config import engine_params
+from .engine import PrismaEngine
+from .records import ST_DESTINATION, ST_DROPPED, ST_PENDING
+from .topology import Topology
+
+
+@dataclass
+class Box:
+    """gym.spaces.Box stand-in (gym is not installed): obs space of one node."""
+    low: int
+    high: int
+    shape: tuple
+    dtype: str = "uint32"
+
+
+@dataclass
+class Discrete:
+    n: int
+
+
+def decode_records(rec: torch.Tensor, W: int) -> dict:
+    """Typed views of gathered records (torch uint8 [n, 32 + 4W] on any device)."""
+    i32 = rec.view(torch.int32)
+    i64 = rec.view(torch.int64)
+    f64 = rec.view(torch.float64)
+    nd = i32[:, 6]
+    w7 = i32[:, 7]
+    act = (w7 & 0xFF)
+    act = torch.where(act >= 128, act - 256, act)
+    return {
+        "t_ns": i64[:, 0], "reward": f64[:, 1], "uid": i32[:, 4], "prev": i32[:, 5],
+        "node": nd & 0xFFFF, "dst": (nd >> 16) & 0xFFFF, "action": act,
+        "status": (w7 >> 8) & 0xFF, "episode": (w7 >> 16) & 0xFFFF, "obs": i32[:, 8:8 + W],
+    }
+
+
+class VecRoutingEnv:
+    def __init__(self, topology="abilene", tm_index: int = 0, load_factor: float = 1.0,
+                 n_replicas: int = 1024, device: int = 0, topo: Optional[Topology] = None, **params):
+        self.topo = topo if topo is not None else Topology.example(topology, tm_index, load_factor)
+        self.params = engine_params(self.topo, **params)
+        self.engine = PrismaEngine(self.topo, self.params, n_replicas, device)
+        self.R = n_replicas
+        self.W = self.engine.W
+        self.device = self.engine.torch_device
+        deg = self.topo.degrees
+        # per-node spaces (data-packet-manager.cc:136-159)
+        self.observation_spaces = [Box(0, 16260, (1 + int(d),)) for d in deg]
+        self.action_spaces = [Discrete(int(d)) for d in deg]
+        self.loss_penalty = float(self.params["loss_penalty"])
+        self._consumed = torch.zeros(self.R, dtype=torch.int64, device=self.device)
+        self._cnt_words = None
+
+    # ------------------------------------------------------------------
+    def reset(self, episode: int = 0):
+        self.engine.reset(episode)
+        self._consumed.zero_()
+        obs, mask, node = self.engine.step(None)
+        return obs, {"mask": mask, "node": node}
+
+    def step(self, actions: torch.Tensor):
+        obs, mask, node = self.engine.step(actions.to(device=self.device, dtype=torch.int32))
+        return obs, {"mask": mask, "node": node}
+
+    def run(self, table: torch.Tensor, max_hops: int):
+        self.engine.run(table, max_hops)
+
+    def counters(self) -> np.ndarray:
+        return self.engine.counters()
+
+    def _dec_counts(self) -> torch.Tensor:
+        words = self.engine.counters_tensor().view(torch.int32)      # [R, 36]
+        from .records import COUNTERS_DTYPE
+        off = COUNTERS_DTYPE.fields["dec_count"][1] // 4
+        return words[:, off].to(torch.int64) & 0xFFFFFFFF
+
+    def transitions(self) -> dict:
+        """Replay transitions completed since the previous call (device tensors).
+
+        For every finalised decision d (not the trailing pending one):
+          - if d has a predecessor p: (obs_p, action_p, reward_d, obs_d, done_d)
+            (forwarder.py:352-379 with signaling_type="ideal");
+          - if d was dropped: (obs_d, action_d, loss_penalty, [dst_d, 0..], True)
+            (forwarder.py:214-240).
+        """
+        W = self.W
+        cap = self.engine.log_capacity
+        dec = self._dec_counts()
+        lo = torch.maximum(self._consumed, dec - cap + 1)
+        n = (dec - lo).clamp_min(0)
+        total = int(n.sum().item())
+        empty = {k: torch.zeros((0,) + s, dtype=t, device=self.device) for k, s, t in
+                 [("obs", (W,), torch.int32), ("action", (), torch.int32), ("reward", (), torch.float64),
+                  ("next_obs", (W,), torch.int32), ("done", (), torch.bool), ("node", (), torch.int32),
+                  ("replica", (), torch.int32)]}
+        if total == 0:
+            return empty
+        rep = torch.repeat_interleave(torch.arange(self.R, device=self.device), n)
+        start = torch.repeat_interleave(lo, n)
+        offs = torch.arange(total, device=self.device) - torch.repeat_interleave(torch.cumsum(n, 0) - n, n)
+        d = start + offs
+        cur = decode_records(self.engine.gather_records(rep.to(torch.int32), d.to(torch.int32)), W)
+        final = cur["status"] != ST_PENDING
+        # consume everything up to (excluding) a trailing pending record
+        last_pending = torch.zeros(self.R, dtype=torch.bool, device=self.device)
+        ends = torch.cumsum(n, 0) - 1
+        has = n > 0
+        last_pending[has] = ~final[ends[has]]
+        self._consumed = torch.where(has, dec - last_pending.to(torch.int64), self._consumed)
+        rep_f, cur_f = rep[final], {k: v[final] for k, v in cur.items()}
+        # hop transitions: predecessor record
+        hp = cur_f["prev"] >= 0
+        prev = decode_records(self.engine.gather_records(rep_f[hp].to(torch.int32), cur_f["prev"][hp].to(torch.int32)), W)
+        # loss transitions
+        dr = cur_f["status"] == ST_DROPPED
+        loss_next = torch.zeros((int(dr.sum()), W), dtype=torch.int32, device=self.device)
+        loss_next[:, 0] = cur_f["obs"][dr][:, 0]
+        out = {
+            "obs": torch.cat([prev["obs"], cur_f["obs"][dr]]),
+            "action": torch.cat([prev["action"], cur_f["action"][dr]]).to(torch.int32),
+            "reward": torch.cat([cur_f["reward"][hp], torch.full((int(dr.sum()),), self.loss_penalty,
+                                                                 dtype=torch.float64, device=self.device)]),
+            "next_obs": torch.cat([cur_f["obs"][hp], loss_next]),
+            "done": torch.cat([cur_f["status"][hp] == ST_DESTINATION,
+                               torch.ones(int(dr.sum()), dtype=torch.bool, device=self.device)]),
+            "node": torch.cat([prev["node"], cur_f["node"][dr]]).to(torch.int32),
+            "replica": torch.cat([rep_f[hp], rep_f[dr]]).to(torch.int32),
+        }
+        return out
+
+    def close(self):
+        self.engine.close()

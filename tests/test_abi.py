@@ -1,0 +1,90 @@
+"""The C-ABI library loads without a GPU and exports exactly what include/prisma.h declares;
+the ctypes mirrors of the ABI structs match the C layout."""
+import ctypes as C
+import os
+import re
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from prisma_amd import engine
+from prisma_amd.records import COUNTERS_DTYPE, record_dtype
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "prisma.h")
+
+
+def declared_functions():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*)\s+(prisma_\w+)\s*\(", txt, re.M)))
+
+
+def test_header_declares_engine_exports():
+    assert declared_functions() == sorted(engine.EXPORTS)
+
+
+def test_library_loads_and_exports_every_symbol():
+    if not os.path.exists(engine.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build_engine()
+    lib = engine.load_library()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.prisma_abi_version() == 1
+    out = subprocess.run(["nm", "-D", "--defined-only", engine.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (prisma_\w+)", out))
+    assert set(declared_functions()) <= exported
+
+
+def test_errors_are_status_codes_not_exits():
+    lib = engine.load_library()
+    h = C.c_void_p()
+    assert lib.prisma_create(None, None, 1, 0, C.byref(h)) == -5          # PRISMA_ERR_ARG
+    assert b"null" in lib.prisma_last_error()
+    assert lib.prisma_reset(None, 0, None) == -5
+    assert lib.prisma_step(None, None, None, None, None, None) == -5
+
+
+C_PROBE = r'''
+#include <stdio.h>
+#include <stddef.h>
+#include "prisma.h"
+int main(void) {
+  printf("%zu %zu %zu %zu\n", sizeof(prisma_topology_t), sizeof(prisma_params_t), sizeof(prisma_counters_t),
+         sizeof(prisma_log_view_t));
+  printf("%zu %zu %zu %zu %zu\n", offsetof(prisma_record_t, obs), offsetof(prisma_params_t, loss_penalty),
+         offsetof(prisma_params_t, log_capacity), offsetof(prisma_counters_t, cost_sum),
+         offsetof(prisma_counters_t, hops_total));
+  return 0;
+}
+'''
+
+
+def test_ctypes_layouts_match_header():
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "probe.c")
+        exe = os.path.join(d, "probe")
+        open(src, "w").write(C_PROBE)
+        subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), src, "-o", exe])
+        lines = subprocess.check_output([exe], text=True).split("\n")
+    sizes = list(map(int, lines[0].split()))
+    offs = list(map(int, lines[1].split()))
+    assert sizes == [C.sizeof(engine._Topo), C.sizeof(engine._Params), COUNTERS_DTYPE.itemsize, C.sizeof(engine._LogView)]
+    assert offs[0] == 32 == record_dtype(4).fields["obs"][1]
+    assert offs[1] == engine._Params.loss_penalty.offset
+    assert offs[2] == engine._Params.log_capacity.offset
+    assert offs[3] == COUNTERS_DTYPE.fields["cost_sum"][1]
+    assert offs[4] == COUNTERS_DTYPE.fields["hops_total"][1]
+
+
+def test_engine_refuses_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from prisma_amd.config import engine_params
+    from prisma_amd.topology import Topology
+    t = Topology.example("abilene")
+    with pytest.raises(engine.PrismaError):
+        engine.PrismaEngine(t, engine_params(t), 4)

@@ -1,0 +1,220 @@
+"""HIP engine vs the CPU oracle on the same seeded inputs (bit-exact), through the C-ABI."""
+import numpy as np
+import pytest
+import torch
+
+from prisma_amd.config import engine_params
+from prisma_amd.engine import PrismaEngine
+from prisma_amd.records import (COUNTERS_DTYPE, ST_DESTINATION, ST_DROPPED, ST_ENQUEUED, ST_PENDING,
+                                transitions)
+from prisma_amd.topology import Topology, sp_next_hop_table
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")]
+
+CNT_KEYS = [k for k in COUNTERS_DTYPE.names if k not in ("hops_total", "events_total")]
+
+
+def assert_counters_equal(g, o, r):
+    bad = [(k, g[k], o[k]) for k in CNT_KEYS if g[k] != o[k]]
+    assert not bad, f"replica {r}: counters differ {bad}"
+
+
+def run_table_both(oracle_mod, topo, params, R, H, table, launches=1, replicas=None):
+    eng = PrismaEngine(topo, params, R)
+    eng.reset(0)
+    t = torch.from_numpy(np.ascontiguousarray(table)).cuda()
+    for _ in range(launches):
+        eng.run(t, H // launches)
+    torch.cuda.synchronize()
+    cnt = eng.counters()
+    log = eng.log_tensor().cpu().numpy()
+    for r in (range(R) if replicas is None else replicas):
+        o = oracle_mod.OracleSim(topo, params, replica=params["replica_base"] + r)
+        o.run_table(table, H)
+        ref = o.records()
+        assert cnt[r]["error"] == 0
+        assert int(cnt[r]["dec_count"]) == len(ref)
+        n = min(len(ref), eng.log_capacity)
+        got = eng.records(r, len(ref) - n, n, log_host=log)
+        assert got.tobytes() == ref[len(ref) - n:].tobytes(), f"replica {r} records differ"
+        assert_counters_equal(cnt[r], o.counters(), r)
+    eng.close()
+    return cnt
+
+
+@pytest.mark.parametrize("name,tm,lf,ping,seed", [
+    ("abilene", 0, 1.0, 1, 100), ("abilene", 0, 1.0, 0, 100), ("abilene", 2, 2.0, 1, 7),
+    ("abilene", 3, 0.5, 0, 12345), ("geant", 0, 1.0, 1, 100), ("geant", 1, 1.5, 0, 3),
+])
+def test_table_policy_parity(oracle_mod, name, tm, lf, ping, seed):
+    topo = Topology.example(name, tm, lf)
+    params = engine_params(topo, sim_time_s=15.0, ping_as_obs=ping, seed=seed, replica_base=5)
+    run_table_both(oracle_mod, topo, params, 6, 2500, sp_next_hop_table(topo))
+
+
+def test_multi_launch_equals_single_launch(oracle_mod):
+    """State staged out to HBM and back between launches changes nothing."""
+    topo = Topology.example("abilene")
+    params = engine_params(topo, sim_time_s=10.0, ping_as_obs=1)
+    run_table_both(oracle_mod, topo, params, 4, 1200, sp_next_hop_table(topo), launches=8)
+
+
+def test_dq_routing_argmin_table_parity(oracle_mod):
+    from prisma_amd.policies import StackedQNet
+    topo = Topology.example("abilene")
+    net = StackedQNet(topo, "routing", seed=11)
+    table = net.argmin_table().cpu().numpy()
+    # the table is exactly the per-decision argmin of the torch model
+    node = torch.arange(11).repeat_interleave(11).cuda()
+    obs = torch.zeros(121, 4, dtype=torch.int32).cuda()
+    obs[:, 0] = torch.arange(11).repeat(11).int().cuda()
+    acts = net.act(obs, node).view(11, 11).cpu().numpy()
+    off = ~np.eye(11, dtype=bool)
+    assert np.array_equal(acts[off], table[off])
+    params = engine_params(topo, sim_time_s=10.0, ping_as_obs=1)
+    run_table_both(oracle_mod, topo, params, 4, 1500, table)
+
+
+def test_external_policy_step_parity(oracle_mod):
+    """Gym-style step(): random actions (2% invalid -> discarded) applied to both."""
+    topo = Topology.example("abilene")
+    params = engine_params(topo, sim_time_s=10.0, ping_as_obs=1)
+    R = 12
+    eng = PrismaEngine(topo, params, R)
+    eng.reset(0)
+    orcs = [oracle_mod.OracleSim(topo, params, replica=r) for r in range(R)]
+    ref_obs = [o.step(-1) for o in orcs]
+    obs, mask, node = eng.step(None)
+    rng = np.random.default_rng(0)
+    deg = topo.degrees
+    for s in range(400):
+        g, m, nd = obs.cpu().numpy(), mask.cpu().numpy(), node.cpu().numpy()
+        acts = np.zeros(R, dtype=np.int32)
+        for r in range(R):
+            assert (ref_obs[r] is None) == (m[r] == 0), (s, r)
+            if ref_obs[r] is None:
+                continue
+            assert np.array_equal(ref_obs[r], g[r]), (s, r, g[r], ref_obs[r])
+            assert nd[r] == int(orcs[r].records()[-1]["node"])
+            acts[r] = rng.integers(0, deg[nd[r]] + (1 if rng.random() < 0.02 else 0))
+        ref_obs = [orcs[r].step(int(acts[r])) for r in range(R)]
+        obs, mask, node = eng.step(torch.from_numpy(acts).cuda())
+    torch.cuda.synchronize()
+    cnt = eng.counters()
+    log = eng.log_tensor().cpu().numpy()
+    for r in range(R):
+        ref = orcs[r].records()
+        assert eng.records(r, 0, len(ref), log_host=log).tobytes() == ref.tobytes()
+        assert_counters_equal(cnt[r], orcs[r].counters(), r)
+    eng.close()
+
+
+def test_episode_end_and_auto_reset(oracle_mod):
+    topo = Topology.example("abilene")
+    base = engine_params(topo, sim_time_s=2.0, ping_as_obs=1)
+    # without auto-reset the episode ends exactly where the oracle's does
+    eng = PrismaEngine(topo, base, 3)
+    eng.reset(0)
+    eng.run(torch.from_numpy(sp_next_hop_table(topo)).cuda(), 10 ** 6)
+    cnt = eng.counters()
+    for r in range(3):
+        o = oracle_mod.OracleSim(topo, base, replica=r)
+        o.run_table(sp_next_hop_table(topo), 10 ** 9)
+        assert cnt[r]["episode_over"] == 1
+        assert_counters_equal(cnt[r], o.counters(), r)
+    eng.close()
+    # with auto-reset, episode 1 equals a fresh oracle episode 1
+    params = dict(base, auto_reset=1)
+    eng = PrismaEngine(topo, params, 2)
+    eng.reset(0)
+    t = torch.from_numpy(sp_next_hop_table(topo)).cuda()
+    eng.run(t, 6000)
+    torch.cuda.synchronize()
+    cnt = eng.counters()
+    log = eng.log_tensor().cpu().numpy()
+    for r in range(2):
+        assert cnt[r]["episode"] >= 1
+        o0 = oracle_mod.OracleSim(topo, base, replica=r, episode=0)
+        o0.run_table(sp_next_hop_table(topo), 10 ** 9)
+        n0 = len(o0.records())
+        o1 = oracle_mod.OracleSim(topo, base, replica=r, episode=1)
+        o1.run_table(sp_next_hop_table(topo), 10 ** 9)
+        ref1 = o1.records()
+        n1 = min(len(ref1), int(cnt[r]["dec_count"]) - n0)
+        got = eng.records(r, n0, n1, log_host=log).copy()
+        assert np.all(got["episode"] == 1)
+        got["prev"] = np.where(got["prev"] >= 0, got["prev"] - n0, got["prev"])
+        assert got.tobytes() == ref1[:n1].tobytes()
+        assert int(cnt[r]["hops_total"]) == 6000
+    eng.close()
+
+
+def test_log_ring_wraps(oracle_mod):
+    topo = Topology.example("abilene")
+    params = engine_params(topo, sim_time_s=10.0, ping_as_obs=0, log_capacity=64)
+    run_table_both(oracle_mod, topo, params, 3, 1000, sp_next_hop_table(topo))
+
+
+def test_small_topologies_and_single_replica(oracle_mod):
+    adj = np.array([[0, 1], [1, 0]])
+    tm = np.array([[0, 900000], [300000, 0]], dtype=object)
+    topo = Topology.from_matrices(adj, tm)
+    params = engine_params(topo, sim_time_s=5.0, ping_as_obs=1)
+    run_table_both(oracle_mod, topo, params, 1, 3000, sp_next_hop_table(topo))
+    ring = np.zeros((6, 6), dtype=int)
+    for i in range(6):
+        ring[i, (i + 1) % 6] = ring[(i + 1) % 6, i] = 1
+    tm = np.full((6, 6), 40000, dtype=object)
+    np.fill_diagonal(tm, 0)
+    topo = Topology.from_matrices(ring, tm)
+    run_table_both(oracle_mod, topo, engine_params(topo, sim_time_s=5.0, ping_as_obs=0), 2, 3000,
+                   sp_next_hop_table(topo))
+
+
+def test_full_size_properties(oracle_mod):
+    """BASELINE size (4096 Abilene replicas): invariants everywhere, 8 replicas checked exactly."""
+    topo = Topology.example("abilene")
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=1)
+    R, H = 4096, 1500
+    rng = np.random.default_rng(3)
+    picks = sorted(rng.choice(R, 8, replace=False).tolist())
+    cnt = run_table_both(oracle_mod, topo, params, R, H, sp_next_hop_table(topo), replicas=picks)
+    assert np.all(cnt["error"] == 0)
+    assert np.all(cnt["hops"] == H)
+    assert np.all(cnt["ov_injected"] >= cnt["ov_arrived"] + cnt["ov_lost"])
+    assert np.all(cnt["cost_n"] == cnt["ov_arrived"] + cnt["ov_lost"])
+    assert np.all(cnt["bytes_data"] == 540 * cnt["ov_injected"])
+    assert len(np.unique(cnt["now_ns"])) > R // 2          # replicas are independent streams
+
+
+def test_vec_env_transitions_match_oracle_join(oracle_mod):
+    from prisma_amd.env import VecRoutingEnv
+    from prisma_amd.policies import SPPolicy
+    R = 8
+    env = VecRoutingEnv("abilene", n_replicas=R, sim_time_s=10.0, ping_as_obs=1)
+    pol = SPPolicy(env.topo)
+    obs, info = env.reset()
+    got = {k: [] for k in ("obs", "action", "reward", "next_obs", "done", "replica")}
+    for _ in range(300):
+        a = pol.act(obs, info["node"].clamp_min(0))
+        obs, info = env.step(a)
+        tr = env.transitions()
+        for k in got:
+            got[k].append(tr[k].cpu().numpy())
+    got = {k: np.concatenate(v) for k, v in got.items()}
+    log = env.engine.log_tensor().cpu().numpy()
+    cnt = env.counters()
+    for r in range(R):
+        recs = env.engine.records(r, 0, int(cnt[r]["dec_count"]), log_host=log)
+        # drop the trailing pending decision, as transitions() does
+        if recs["status"][-1] == ST_PENDING:
+            recs = recs[:-1]
+        ref = transitions(recs, env.loss_penalty)
+        sel = got["replica"] == r
+        key = lambda o, a, rw, no, d: sorted(zip(map(tuple, o.tolist()), a.tolist(), rw.tolist(),
+                                                 map(tuple, no.tolist()), d.tolist()))
+        assert key(got["obs"][sel].astype(np.uint32), got["action"][sel], got["reward"][sel],
+                   got["next_obs"][sel].astype(np.uint32), got["done"][sel]) == \
+            key(ref["obs"], ref["action"], ref["reward"], ref["next_obs"], ref["done"])
+    env.close()
