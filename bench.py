@@ -1,0 +1,214 @@
+"""Headline benchmark: packet-hop transitions/s at 4096 Abilene replicas per MI355X.
+
+Workload (BASELINE.json configs[1]): Abilene TM0, load_factor 1.0, DQ-Routing
+agent (per-node DQN_routing_model restated in torch, random-init weights from
+a fixed seed, greedy argmin -> exact [N, N] action table), pingAsObs=1,
+train=0, simTime 60 s with auto-reset, 4096 replicas per GPU.
+One step = refresh the policy table from the torch model (the agent's
+forward pass over every (node, dst)) + one engine launch in which every
+replica executes `--hops` forwarding decisions (enqueue or drop), logging
+one decision record per data notification to HBM.
+
+Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
+torch.distributed.run (one process per GPU, RCCL); replicas are sharded
+(weak scaling: replica ids rank*R .. rank*R+R-1), no data-path collective;
+the per-replica episode statistics are all-gathered over RCCL at the end.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "packet-hop transitions/sec at 4096 Abilene replicas; achieved HBM GB/s"
+HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--replicas", type=int, default=4096, help="replicas per GPU")
+    p.add_argument("--hops", type=int, default=2048, help="hops per replica per step")
+    p.add_argument("--topology", default="abilene")
+    p.add_argument("--tm", type=int, default=0)
+    p.add_argument("--load-factor", type=float, default=1.0)
+    p.add_argument("--ping-as-obs", type=int, default=1)
+    p.add_argument("--cpu-baseline", type=int, default=1)
+    p.add_argument("--cpu-hops", type=int, default=1000000, help="oracle hops per sampled replica")
+    return p.parse_args()
+
+
+def algorithmic_bytes(hops: int, deg_sum: int) -> int:
+    """B_hop(u) = 85 + 12*deg(u) bytes, summed over executed hops."""
+    return 85 * hops + 12 * deg_sum
+
+
+def cpu_baseline(topo, params, table, hops_per_replica: int):
+    """The C oracle (oracle/, kind 'port') on host threads, one replica per thread."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    O.build()
+    cores = max(1, min(16, os.cpu_count() or 1))
+    sims = [O.OracleSim(topo, params, replica=100000 + i) for i in range(cores)]
+    done = [0] * cores
+
+    def work(i):
+        done[i] = sims[i].run_table(table, hops_per_replica)   # ctypes releases the GIL
+
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(cores)]
+    t0 = time.perf_counter()
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    dt = time.perf_counter() - t0
+    for s in sims:
+        s.close()
+    hops = int(sum(done))
+    return {"value": hops / dt, "unit": "hops/s", "cores": cores, "kind": "port",
+            "sample": f"{cores} Abilene replicas x {hops_per_replica} hops (same params and DQ-routing table), "
+                      f"one replica per host thread, {dt:.2f} s wall; ns-3 reference path not runnable (SURVEY 8c)"}
+
+
+def pmc_traffic(replicas: int, hops: int):
+    """HBM bytes per launch from the committed rocprofv3 --pmc passes (profiles/pmc_traffic.json)."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as fh:
+            d = json.load(fh)
+        if int(d.get("replicas", -1)) == replicas and int(d.get("hops", -1)) == hops:
+            return float(d["bytes_per_launch"])
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from prisma_amd.config import engine_params
+    from prisma_amd.dist import gather_replica_stats, shard
+    from prisma_amd.engine import PrismaEngine
+    from prisma_amd.policies import StackedQNet
+    from prisma_amd.topology import Topology
+
+    topo = Topology.example(args.topology, args.tm, args.load_factor)
+    base, R = shard(args.replicas * world, rank, world)
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=args.ping_as_obs, auto_reset=1,
+                           replica_base=base, seed=100)
+    eng = PrismaEngine(topo, params, R, device=local)
+    agent = StackedQNet(topo, "routing", seed=1234, device=dev)
+
+    def step():
+        table = agent.argmin_table()              # policy forward for every (node, dst)
+        eng.run(table, args.hops)
+
+    eng.reset(0)
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    c0 = eng.counters()
+    stream = torch.cuda.current_stream()
+    evs = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        table = agent.argmin_table()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        eng.run(table, args.hops)
+        e1.record(stream)
+        evs.append((e0, e1))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    c1 = eng.counters()
+    hops_local = int((c1["hops_total"] - c0["hops_total"]).sum())
+    deg_avg = float(c1["hop_deg_sum"].sum()) / max(1, int(c1["hops"].sum()))   # mean deg(u) over hops
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    errors = int(c1["error"].max())
+    stats = gather_replica_stats(c1, world)                    # RCCL all-gather (outside the timed region)
+    hops_total = hops_local
+    if world > 1:
+        ht = torch.tensor([hops_local], dtype=torch.int64, device=dev)
+        dist.all_reduce(ht)
+        hops_total = int(ht.item())
+
+    if rank == 0:
+        # per-launch algorithmic bytes: the hops one launch executes on this rank x B_hop at their mean degree
+        hops_per_launch = hops_local / args.steps
+        alg_bytes = algorithmic_bytes(int(round(hops_per_launch)), int(round(hops_per_launch * deg_avg)))
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = pmc_traffic(args.replicas, args.hops)
+        result = {
+            "metric": METRIC,
+            "value": hops_total / elapsed,
+            "unit": "hops/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (Poisson traffic from the shipped Abilene TM0; random-init DQ-routing weights)",
+            "config": {
+                "workload": f"{args.topology} tm{args.tm} lf{args.load_factor} dq_routing greedy, "
+                            f"{args.replicas} replicas/GPU x {args.hops} hops/step, pingAsObs={args.ping_as_obs}, "
+                            f"simTime 60 s auto-reset",
+                "topology": args.topology, "replicas_per_gpu": args.replicas, "hops_per_step": args.hops,
+                "policy": "dq_routing", "parallelism": f"replica-sharded x{world}",
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": "prisma_step_kernel", "kernel_ms": kern_ms,
+                "alg_bytes_per_launch": alg_bytes, "hops_per_launch": hops_per_launch,
+            },
+            "errors": errors,
+            "episodes_completed": stats["episodes_completed"],
+        }
+        if args.cpu_baseline and world == 1:
+            result["cpu_baseline"] = cpu_baseline(topo, dict(params, auto_reset=0),
+                                                  agent.argmin_table().cpu().numpy(), args.cpu_hops)
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

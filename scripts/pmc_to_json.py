@@ -1,0 +1,39 @@
+"""Turn a profile_round.sh output dir into profiles/<tag>/ summaries + profiles/pmc_traffic.json.
+
+HBM bytes per launch of prisma_step_kernel = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
+(MI355X_MICROARCH.md 'HBM': FETCH_SIZE counts half the bytes of wide coalesced reads on
+gfx950 — our staging reads are 16 B/lane; WRITE_SIZE is exact for 16-B stores, our
+record stores are 4-8 B and are reported as measured, uncalibrated).
+"""
+import csv, json, os, shutil, statistics, sys
+
+src, tag = sys.argv[1], sys.argv[2]
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+dst = os.path.join(root, "profiles", tag)
+os.makedirs(dst, exist_ok=True)
+
+
+def vals(path, counter):
+    rows = [r for r in csv.DictReader(open(path)) if r["Kernel_Name"] == "prisma_step_kernel" and r["Counter_Name"] == counter]
+    return [float(r["Counter_Value"]) for r in rows]
+
+
+fetch = vals(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE")
+write = vals(os.path.join(src, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE")
+bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlines()[-1])
+cfg = bench["config"]
+f_kb, w_kb = statistics.median(fetch[1:] or fetch), statistics.median(write[1:] or write)
+out = {
+    "kernel": "prisma_step_kernel", "replicas": cfg["replicas_per_gpu"], "hops": cfg["hops_per_step"],
+    "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
+    "read_bytes_per_launch": 2 * f_kb * 1024, "write_bytes_per_launch": w_kb * 1024,
+    "bytes_per_launch": 2 * f_kb * 1024 + w_kb * 1024,
+    "correction": "read x2 (gfx950 FETCH_SIZE half-count for 16-B/lane streaming reads); writes as measured",
+    "dispatches": len(fetch), "tag": tag,
+}
+json.dump(out, open(os.path.join(root, "profiles", "pmc_traffic.json"), "w"), indent=1)
+shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
+shutil.copy(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), os.path.join(dst, "pmc_fetch_size.csv"))
+shutil.copy(os.path.join(src, "pmc_write", "run_counter_collection.csv"), os.path.join(dst, "pmc_write_size.csv"))
+shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
+print(json.dumps(out, indent=1))
