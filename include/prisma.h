@@ -125,8 +125,8 @@ typedef struct prisma_params {
  * reward is the reference's hop_time_real = curr_time - t_decision computed
  * on the microsecond-formatted times (packet-manager.cc:127-128 ->
  * forwarder.py:208,360), bit-identical to the Python float.
- * Record size is 32 + 4 * obs_width bytes (obs_width = 1 + max_deg rounded
- * up to even).
+ * Record size is 32 + 4 * obs_width bytes (obs_width = 1 + max_deg rounded up
+ * to a multiple of 4, so records are whole 16-byte rows).
  */
 typedef struct prisma_record {
     int64_t  t_ns;

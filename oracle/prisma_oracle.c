@@ -663,7 +663,7 @@ or_sim_t* or_create(const or_config_t* cfg) {
     or_sim_t* s = calloc(1, sizeof(or_sim_t));
     s->c = *cfg;
     s->N = cfg->n_nodes; s->E = cfg->n_links; s->F = cfg->n_flows;
-    int w = 1 + cfg->max_deg; s->W = w + (w & 1);
+    s->W = (1 + cfg->max_deg + 3) & ~3;                 /* multiple of 4 (16-B rows) */
     s->rec_bytes = (int)sizeof(rec_head_t) + 4 * s->W;
     s->t_end = or_seconds_to_ns(cfg->sim_time_s);
     s->ping_period = or_seconds_to_ns((double)cfg->ping_interval_s);

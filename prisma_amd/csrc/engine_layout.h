@@ -74,10 +74,12 @@ struct Layout {
     int32_t N, E, L, F, W, max_deg, WCAP, MA;
     uint32_t topo_bytes, state_bytes, lds_bytes, table_bytes;
     // topology image (LDS offset 0)
-    uint32_t t_rowptr, t_ldst, t_lrev, t_lfrom, t_txd, t_txp, t_prop, t_rofs, t_rcap, t_qmax,
-             t_fsrc, t_fdst, t_fmean, t_table;
+    uint32_t t_rowptr, t_ldst, t_lrev, t_acctx, t_fsrc, t_fdst, t_fmean, t_table;
     // state image (LDS offset topo_bytes)
-    uint32_t s_hdr, s_cnt, s_obs, s_ft, s_fseq, s_fdraw, s_link, s_wt, s_wseq, s_ring, s_win, s_pmeta;
+    uint32_t s_hdr, s_cnt, s_obs, s_fkey, s_fdraw, s_lkey, s_link, s_wt, s_wseq, s_ring, s_win, s_pmeta;
+    // link constants (identical on every switch link: sim.cc:414-433)
+    int64_t  sw_txd, sw_txp, sw_prop;
+    uint32_t qcap_s, qcap_a, qmax_bytes, acc_qmax_pkts;
     // scenario constants
     int64_t  t_end, ping_period;
     uint32_t data_size, ping_size;

@@ -139,20 +139,37 @@ struct KParams {
     int32_t mode;                // 0 reset, 1 external step, 2 table run
 };
 
+// candidate key of one event source: 16 bytes, read with one ds_read_b128
+struct __attribute__((aligned(16))) CKey {
+    int64_t  t;
+    uint32_t seq;
+    uint32_t code;               // kind << 28 | index
+};
+
+// Lane-0 scalar state kept in registers for the whole event loop; it is
+// loaded from / stored to the Hdr + counters of the LDS image at the loop
+// boundaries only.
+struct Hot {
+    int64_t  now, ping_t;
+    uint32_t ping_seq, seq, uid, dec, ping_rounds, episode;
+    uint32_t pend, over, error, stop, hops_launch;
+    uint64_t hops_total, events_total;
+    prisma_counters_t c;
+};
+
 struct Sim {
     const Layout* L;
     unsigned char* base;         // LDS base
     Hdr* h;
     prisma_counters_t* c;
     uint32_t* obs;
-    int64_t* ft; uint32_t* fseq; uint32_t* fdraw;
-    LinkState* ln;
+    CKey* fkey; uint32_t* fdraw;
+    CKey* lkey; LinkState* ln;
     int64_t* wt; uint32_t* wseq;
     uint4* ring;
     float* win; PingMeta* pm;
-    const int32_t* rowptr; const int32_t* ldst; const int32_t* lrev; const int32_t* lfrom;
-    const int64_t* txd; const int64_t* txp; const int64_t* prop;
-    const uint32_t* rofs; const uint32_t* rcap; const uint32_t* qmax;
+    const int32_t* rowptr; const int32_t* ldst; const int32_t* lrev;
+    const int64_t* acctx;
     const int32_t* fsrc; const int32_t* fdst; const double* fmean;
     const uint8_t* table;
     unsigned char* logrep;       // this replica's log ring (HBM)
@@ -166,9 +183,9 @@ __device__ inline void sim_bind(Sim& S, const Layout& L, unsigned char* lds, uns
     S.h = (Hdr*)(st + L.s_hdr);
     S.c = (prisma_counters_t*)(st + L.s_cnt);
     S.obs = (uint32_t*)(st + L.s_obs);
-    S.ft = (int64_t*)(st + L.s_ft);
-    S.fseq = (uint32_t*)(st + L.s_fseq);
+    S.fkey = (CKey*)(st + L.s_fkey);
     S.fdraw = (uint32_t*)(st + L.s_fdraw);
+    S.lkey = (CKey*)(st + L.s_lkey);
     S.ln = (LinkState*)(st + L.s_link);
     S.wt = (int64_t*)(st + L.s_wt);
     S.wseq = (uint32_t*)(st + L.s_wseq);
@@ -178,13 +195,7 @@ __device__ inline void sim_bind(Sim& S, const Layout& L, unsigned char* lds, uns
     S.rowptr = (const int32_t*)(lds + L.t_rowptr);
     S.ldst = (const int32_t*)(lds + L.t_ldst);
     S.lrev = (const int32_t*)(lds + L.t_lrev);
-    S.lfrom = (const int32_t*)(lds + L.t_lfrom);
-    S.txd = (const int64_t*)(lds + L.t_txd);
-    S.txp = (const int64_t*)(lds + L.t_txp);
-    S.prop = (const int64_t*)(lds + L.t_prop);
-    S.rofs = (const uint32_t*)(lds + L.t_rofs);
-    S.rcap = (const uint32_t*)(lds + L.t_rcap);
-    S.qmax = (const uint32_t*)(lds + L.t_qmax);
+    S.acctx = (const int64_t*)(lds + L.t_acctx);
     S.fsrc = (const int32_t*)(lds + L.t_fsrc);
     S.fdst = (const int32_t*)(lds + L.t_fdst);
     S.fmean = (const double*)(lds + L.t_fmean);
@@ -193,73 +204,121 @@ __device__ inline void sim_bind(Sim& S, const Layout& L, unsigned char* lds, uns
     S.gid = gid;
 }
 
-__device__ inline void fail(Sim& S, uint32_t bit) {
-    S.h->error |= bit;
-    S.h->over = 1;
-    S.h->stop = 1;
+__device__ inline void hot_load(const Sim& S, Hot& H) {
+    const Hdr& h = *S.h;
+    H.now = h.now; H.ping_t = h.ping_t; H.ping_seq = h.ping_seq; H.seq = h.seq; H.uid = h.uid;
+    H.dec = h.dec_count; H.ping_rounds = h.ping_rounds; H.episode = h.episode; H.pend = h.pend;
+    H.over = h.over; H.error = h.error; H.stop = h.stop; H.hops_launch = h.hops_launch;
+    H.hops_total = h.hops_total; H.events_total = h.events_total;
+    H.c = *S.c;
+}
+
+__device__ inline void hot_store(Sim& S, const Hot& H) {
+    Hdr& h = *S.h;
+    h.now = H.now; h.ping_t = H.ping_t; h.ping_seq = H.ping_seq; h.seq = H.seq; h.uid = H.uid;
+    h.dec_count = H.dec; h.ping_rounds = H.ping_rounds; h.episode = H.episode; h.pend = H.pend;
+    h.over = H.over; h.error = H.error; h.stop = H.stop; h.hops_launch = H.hops_launch;
+    h.hops_total = H.hops_total; h.events_total = H.events_total;
+    prisma_counters_t c = H.c;
+    c.now_ns = H.now; c.episode = H.episode; c.ping_rounds = H.ping_rounds; c.seq = H.seq; c.uid = H.uid;
+    c.dec_count = H.dec; c.error = H.error; c.episode_over = H.over;
+    c.hops_total = H.hops_total; c.events_total = H.events_total;
+    *S.c = c;
+}
+
+__device__ inline void fail(Hot& H, uint32_t bit) {
+    H.error |= bit;
+    H.over = 1;
+    H.stop = 1;
+}
+
+__device__ inline bool key_less(int64_t t, uint32_t s, int64_t bt, uint32_t bs) {
+    return t < bt || (t == bt && s < bs);
 }
 
 // ---- link FIFO / transmitter (point-to-point-net-device.cc:273-336, 595-666)
-__device__ inline uint32_t ent_size(const Sim& S, uint32_t x) {
-    return ent_type(x) == T_DATA ? S.L->data_size : S.L->ping_size;
+__device__ inline uint32_t ent_size(const Layout& L, uint32_t x) {
+    return ent_type(x) == T_DATA ? L.data_size : L.ping_size;
+}
+__device__ inline uint32_t ring_off(const Layout& L, int l) {
+    return l < L.E ? (uint32_t)l * L.qcap_s : (uint32_t)L.E * L.qcap_s + (uint32_t)(l - L.E) * L.qcap_a;
+}
+__device__ inline uint32_t ring_cap(const Layout& L, int l) { return l < L.E ? L.qcap_s : L.qcap_a; }
+
+// recompute the candidate key of link l: next tx completion or wire head
+__device__ inline void relink(Sim& S, int l) {
+    const LinkState& k = S.ln[l];
+    CKey key;
+    key.t = INT64_MAX; key.seq = 0xffffffffu; key.code = 0xffffffffu;
+    if (k.busy) { key.t = k.complete_t; key.seq = k.complete_seq; key.code = (K_COMPLETE << 28) | (uint32_t)l; }
+    if (k.n_wire) {
+        uint32_t w = (uint32_t)l * S.L->WCAP + ((uint32_t)k.head & (uint32_t)(S.L->WCAP - 1));
+        int64_t t = S.wt[w]; uint32_t s = S.wseq[w];
+        if (key_less(t, s, key.t, key.seq)) { key.t = t; key.seq = s; key.code = (K_ARRIVE << 28) | (uint32_t)l; }
+    }
+    S.lkey[l] = key;
 }
 
-__device__ inline void transmit_start(Sim& S, int l, uint32_t ring_idx, uint32_t x) {
+__device__ inline void transmit_start(Sim& S, Hot& H, int l, uint32_t ring_idx, uint32_t x) {
+    const Layout& L = *S.L;
     LinkState& k = S.ln[l];
-    int64_t now = S.h->now;
-    int64_t tx = ent_type(x) == T_DATA ? S.txd[l] : S.txp[l];
+    int64_t tx = l < L.E ? (ent_type(x) == T_DATA ? L.sw_txd : L.sw_txp) : S.acctx[l - L.E];
+    int64_t prop = l < L.E ? L.sw_prop : 0;
     k.busy = 1;
-    k.complete_t = now + tx;
-    k.complete_seq = S.h->seq++;                               // TransmitComplete
-    uint32_t w = (uint32_t)l * S.L->WCAP + (ring_idx & (uint32_t)(S.L->WCAP - 1));
-    S.wt[w] = now + tx + S.prop[l];
-    S.wseq[w] = S.h->seq++;                                    // channel Receive
-    if (k.n_wire > (uint32_t)S.L->WCAP) fail(S, PRISMA_EBIT_WIRE);
+    k.complete_t = H.now + tx;
+    k.complete_seq = H.seq++;                                  // TransmitComplete
+    uint32_t w = (uint32_t)l * L.WCAP + (ring_idx & (uint32_t)(L.WCAP - 1));
+    S.wt[w] = H.now + tx + prop;
+    S.wseq[w] = H.seq++;                                       // channel Receive
+    if (k.n_wire > (uint32_t)L.WCAP) fail(H, PRISMA_EBIT_WIRE);
 }
 
-// returns 1 if enqueued, 0 if dropped
-__device__ inline int link_send(Sim& S, int l, uint4 e) {
+// returns 1 if enqueued, 0 if dropped (or on ring overflow, which fails the replica)
+__device__ inline int link_send(Sim& S, Hot& H, int l, uint4 e) {
+    const Layout& L = *S.L;
     LinkState& k = S.ln[l];
-    uint32_t size = ent_size(S, e.x);
-    uint32_t qm = S.qmax[l];
-    bool ok = (qm & 0x80000000u) ? ((uint32_t)k.n_queue + 1u <= (qm & 0x7fffffffu))
-                                 : (k.q_bytes + size <= qm);
+    uint32_t size = ent_size(L, e.x);
+    bool ok = l < L.E ? (k.q_bytes + size <= L.qmax_bytes) : ((uint32_t)k.n_queue + 1u <= L.acc_qmax_pkts);
     if (!ok) return 0;
-    uint32_t cap = S.rcap[l];
-    if ((uint32_t)k.n_wire + k.n_queue + 1u > cap) { fail(S, PRISMA_EBIT_RING); return 0; }
+    uint32_t cap = ring_cap(L, l), off = ring_off(L, l);
+    if ((uint32_t)k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
     uint32_t ti = k.tail;
-    S.ring[S.rofs[l] + ti] = e;
+    S.ring[off + ti] = e;
     k.tail = (uint16_t)(ti + 1 == cap ? 0 : ti + 1);
     k.n_queue++;
     k.q_bytes += size;
     if (!k.busy) {                                              // :643-650
         uint32_t xi = k.txp;
-        uint4 h = S.ring[S.rofs[l] + xi];
+        uint4 hd = S.ring[off + xi];
         k.txp = (uint16_t)(xi + 1 == cap ? 0 : xi + 1);
         k.n_queue--;
         k.n_wire++;
-        k.q_bytes -= ent_size(S, h.x);
-        transmit_start(S, l, xi, h.x);
+        k.q_bytes -= ent_size(L, hd.x);
+        transmit_start(S, H, l, xi, hd.x);
+        relink(S, l);
     }
     return 1;
 }
 
-__device__ inline void on_complete(Sim& S, int l) {                 // :305-336
+__device__ inline void on_complete(Sim& S, Hot& H, int l) {         // :305-336
+    const Layout& L = *S.L;
     LinkState& k = S.ln[l];
     k.busy = 0;
-    if (k.n_queue == 0) return;
-    uint32_t cap = S.rcap[l];
-    uint32_t xi = k.txp;
-    uint4 h = S.ring[S.rofs[l] + xi];
-    k.txp = (uint16_t)(xi + 1 == cap ? 0 : xi + 1);
-    k.n_queue--;
-    k.n_wire++;
-    k.q_bytes -= ent_size(S, h.x);
-    transmit_start(S, l, xi, h.x);
+    if (k.n_queue) {
+        uint32_t cap = ring_cap(L, l);
+        uint32_t xi = k.txp;
+        uint4 hd = S.ring[ring_off(L, l) + xi];
+        k.txp = (uint16_t)(xi + 1 == cap ? 0 : xi + 1);
+        k.n_queue--;
+        k.n_wire++;
+        k.q_bytes -= ent_size(L, hd.x);
+        transmit_start(S, H, l, xi, hd.x);
+    }
+    relink(S, l);
 }
 
 // ---- observation (data-packet-manager.cc:171-206)
-__device__ inline uint32_t ping_value(const Sim& S, int l) {
+__device__ inline uint32_t ping_value(const Sim& S, const Hot& H, int l) {
     const PingMeta& m = S.pm[l];
     double avg = 0.0;
     if (m.win_n > 0) {
@@ -278,11 +337,11 @@ __device__ inline uint32_t ping_value(const Sim& S, int l) {
     // after the last ack if it was sent.
     int64_t oldest = -1;
     if (m.first_hole >= 0) oldest = m.first_hole;
-    else if ((int64_t)m.acked_last + 1 < (int64_t)S.h->ping_rounds) oldest = (int64_t)m.acked_last + 1;
+    else if ((int64_t)m.acked_last + 1 < (int64_t)H.ping_rounds) oldest = (int64_t)m.acked_last + 1;
     float mt = 0.0f;
     if (oldest >= 0) {
         uint64_t ms = (uint64_t)(((oldest + 1) * S.L->ping_period) / 1000000);
-        double a = ns_to_sec(S.h->now) - (double)ms * 0.001;
+        double a = ns_to_sec(H.now) - (double)ms * 0.001;
         double b = 2.60;
         mt = (float)((b < a) ? b : a);
     }
@@ -290,62 +349,65 @@ __device__ inline uint32_t ping_value(const Sim& S, int l) {
     return (uint32_t)(1000 * mx);
 }
 
-__device__ inline void observe(Sim& S, int v, uint32_t dst) {
+__device__ inline void observe(Sim& S, const Hot& H, int v, uint32_t dst) {
     const int W = S.L->W;
-    for (int i = 0; i < W; ++i) S.obs[i] = 0;
-    S.obs[0] = dst;
     int r0 = S.rowptr[v], r1 = S.rowptr[v + 1];
-    for (int l = r0; l < r1; ++l)
-        S.obs[1 + l - r0] = S.L->ping_as_obs ? ping_value(S, l) : S.ln[l].q_bytes;
+    S.obs[0] = dst;
+    for (int i = 1; i < W; ++i) {
+        int l = r0 + i - 1;
+        S.obs[i] = l < r1 ? (S.L->ping_as_obs ? ping_value(S, H, l) : S.ln[l].q_bytes) : 0u;
+    }
 }
 
 __device__ inline unsigned char* rec_ptr(const Sim& S, uint32_t d) {
     return S.logrep + (size_t)(d & (S.L->log_cap - 1)) * S.L->rec_bytes;
 }
 
-__device__ inline void write_record(Sim& S, uint32_t d, int64_t t, double reward, uint32_t uid, int32_t prev,
+__device__ inline void write_record(Sim& S, const Hot& H, uint32_t d, double reward, uint32_t uid, int32_t prev,
                                     uint32_t node, uint32_t dst, int action, uint32_t status) {
     unsigned char* p = rec_ptr(S, d);
-    *(int64_t*)(p + 0) = t;
-    *(double*)(p + 8) = reward;
-    *(uint32_t*)(p + 16) = uid;
-    *(int32_t*)(p + 20) = prev;
-    *(uint32_t*)(p + 24) = node | (dst << 16);
-    *(uint32_t*)(p + 28) = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((S.h->episode & 0xffffu) << 16);
-    uint32_t* o = (uint32_t*)(p + 32);
-    for (int i = 0; i < S.L->W; ++i) o[i] = S.obs[i];
+    uint4 a, b;
+    a.x = (uint32_t)H.now; a.y = (uint32_t)((uint64_t)H.now >> 32);
+    uint64_t rb = __double_as_longlong(reward);
+    a.z = (uint32_t)rb; a.w = (uint32_t)(rb >> 32);
+    b.x = uid; b.y = (uint32_t)prev; b.z = node | (dst << 16);
+    b.w = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
+    *(uint4*)(p + 0) = a;
+    *(uint4*)(p + 16) = b;
+    const uint4* o = (const uint4*)S.obs;
+    for (int i = 0; i < S.L->W / 4; ++i) ((uint4*)(p + 32))[i] = o[i];
+    if (S.L->W & 2) *(uint2*)(p + 32 + 16 * (S.L->W / 4)) = *(const uint2*)(S.obs + 4 * (S.L->W / 4));
 }
 
-__device__ inline void patch_record(Sim& S, uint32_t d, int action, uint32_t status) {
+__device__ inline void patch_record(Sim& S, const Hot& H, uint32_t d, int action, uint32_t status) {
     unsigned char* p = rec_ptr(S, d);
-    *(uint32_t*)(p + 28) = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((S.h->episode & 0xffffu) << 16);
+    *(uint32_t*)(p + 28) = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
 }
 
 // Receive tail after the MacRx trace (point-to-point-net-device.cc:430-463)
-__device__ inline void receive_counters(Sim& S, uint32_t x, int v) {
-    prisma_counters_t& c = *S.c;
+__device__ inline void receive_counters(const Layout& L, Hot& H, uint32_t x, int v) {
+    prisma_counters_t& c = H.c;
     uint32_t type = ent_type(x);
     if (type == T_DATA && ent_dst(x) == (uint32_t)v) {
         // valable, nextHop == finalDest on identity overlays
         c.ov_arrived++;
-        float cost = (float)(ns_to_sec(S.h->now) - (double)ent_aux(x));
+        float cost = (float)(ns_to_sec(H.now) - (double)ent_aux(x));
         c.cost_sum += cost; c.cost_n++;
         c.e2e_sum += cost; c.e2e_n++;
     }
-    if (type > 0 && ent_dst(x) == (uint32_t)v) c.bytes_signaling += (int32_t)(S.L->ping_size - 2);
+    if (type > 0 && ent_dst(x) == (uint32_t)v) c.bytes_signaling += (int32_t)(L.ping_size - 2);
     if (type == T_DATA && ent_fresh(x)) {
         c.ov_injected++;
-        c.bytes_data += (int32_t)(S.L->data_size - 2);
+        c.bytes_data += (int32_t)(L.data_size - 2);
     }
 }
 
 // DataPacketManager::sendPacket (data-packet-manager.cc:251-299) for the
-// pending decision, then the Receive tail.
-__device__ inline void finish_decision(Sim& S, int action) {
-    Hdr& h = *S.h;
-    int v = (int)h.pend_node;
-    uint32_t d = h.pend_dec;
-    uint4 e = make_uint4(h.pend_ent[0], h.pend_ent[1], h.pend_ent[2], h.pend_ent[3]);
+// decision held in (e, v, d), then the Receive tail.  `fused` = the record
+// was not written yet (table policy: one record write per decision).
+__device__ inline void apply_decision(Sim& S, Hot& H, uint4 e, int v, uint32_t d, int action, bool fused,
+                                      double reward, int32_t prev) {
+    const Layout& L = *S.L;
     int r0 = S.rowptr[v], deg = S.rowptr[v + 1] - r0;
     uint32_t status;
     if (action >= 0 && action < deg) {
@@ -354,33 +416,40 @@ __device__ inline void finish_decision(Sim& S, int action) {
         f.x = ent_make(T_DATA, ent_src(e.x), ent_dst(e.x), 0u, 1u, ent_aux(e.x));
         f.y = e.y;                                   // uid
         f.z = d;                                     // decision of this hop
-        f.w = (uint32_t)py_micros(h.now);            // temp_obs time
-        S.c->hops++;
-        S.c->hop_deg_sum += (uint64_t)deg;
-        if (link_send(S, l, f)) {
+        f.w = (uint32_t)py_micros(H.now);            // temp_obs time
+        H.c.hops++;
+        H.c.hop_deg_sum += (uint64_t)deg;
+        if (link_send(S, H, l, f)) {
             status = PRISMA_ST_ENQUEUED;
         } else {
             status = PRISMA_ST_DROPPED;              // :655-664 + forwarder.py:214-244
-            S.c->ov_lost++;
-            S.c->cost_sum += S.L->loss_penalty_f;
-            S.c->cost_n++;
-            S.c->reward_sum += S.L->loss_penalty;
+            H.c.ov_lost++;
+            H.c.cost_sum += L.loss_penalty_f;
+            H.c.cost_n++;
+            H.c.reward_sum += L.loss_penalty;
         }
     } else {
         status = PRISMA_ST_DISCARDED;
     }
-    patch_record(S, d, action, status);
-    receive_counters(S, e.x, v);
-    h.pend = 0;
+    if (fused) write_record(S, H, d, reward, e.y, prev, (uint32_t)v, ent_dst(e.x), action, status);
+    else patch_record(S, H, d, action, status);
+    receive_counters(L, H, e.x, v);
+}
+
+__device__ inline void finish_pending(Sim& S, Hot& H, int action) {
+    Hdr& h = *S.h;
+    uint4 e = make_uint4(h.pend_ent[0], h.pend_ent[1], h.pend_ent[2], h.pend_ent[3]);
+    apply_decision(S, H, e, (int)h.pend_node, h.pend_dec, action, false, 0.0, 0);
+    H.pend = 0;
 }
 
 // ---- handlers (lane 0) ------------------------------------------------------
-__device__ inline void on_ping_round(Sim& S) {                      // data-packet-manager.cc:350-413
-    Hdr& h = *S.h;
-    uint32_t k = h.ping_rounds;
-    uint32_t ms = (uint32_t)(h.now / 1000000);
+__device__ inline void on_ping_round(Sim& S, Hot& H) {              // data-packet-manager.cc:350-413
+    const Layout& L = *S.L;
+    uint32_t k = H.ping_rounds;
+    uint32_t ms = (uint32_t)(H.now / 1000000);
     uint32_t first_rearm = 0;
-    for (int u = 0; u < S.L->N; ++u) {
+    for (int u = 0; u < L.N; ++u) {
         int r0 = S.rowptr[u], r1 = S.rowptr[u + 1];
         for (int l = r0; l < r1; ++l) {
             uint4 e;
@@ -388,100 +457,101 @@ __device__ inline void on_ping_round(Sim& S) {                      // data-pack
             e.y = k;
             e.z = ms;
             e.w = 0;
-            if (!link_send(S, l, e)) S.c->ctrl_dropped++;
+            if (!link_send(S, H, l, e)) H.c.ctrl_dropped++;
         }
-        uint32_t s = h.seq++;                                    // re-arm of node u
+        uint32_t s = H.seq++;                                    // re-arm of node u
         if (u == 0) first_rearm = s;
     }
-    h.ping_rounds = k + 1;
+    H.ping_rounds = k + 1;
     // one ns-3 event per node timer (the round is N consecutive events)
-    S.c->events += (uint64_t)(S.L->N - 1);
-    h.events_total += (uint64_t)(S.L->N - 1);
-    h.ping_t = h.now + S.L->ping_period;
-    h.ping_seq = first_rearm;
+    H.c.events += (uint64_t)(L.N - 1);
+    H.events_total += (uint64_t)(L.N - 1);
+    H.ping_t = H.now + L.ping_period;
+    H.ping_seq = first_rearm;
 }
 
-__device__ inline void flow_next(Sim& S, int f) {                   // poisson-application.cc:265-295
-    uint32_t c[4] = { (uint32_t)f, S.fdraw[f], S.h->episode, 1u };
+__device__ inline void flow_next(Sim& S, Hot& H, int f) {           // poisson-application.cc:265-295
+    uint32_t draw = S.fdraw[f];
+    uint32_t c[4] = { (uint32_t)f, draw, H.episode, 1u };
     philox4x32_10(c, S.L->seed_lo, S.gid);
     uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
     double U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
     double delay = -S.fmean[f] * det_log(U);
-    S.fdraw[f]++;
-    S.ft[f] = S.h->now + sec_to_ns(delay);
-    S.fseq[f] = S.h->seq++;
+    S.fdraw[f] = draw + 1;
+    CKey key;
+    key.t = H.now + sec_to_ns(delay);
+    key.seq = H.seq++;
+    key.code = (K_FLOW << 28) | (uint32_t)f;
+    S.fkey[f] = key;
 }
 
-__device__ inline void on_flow(Sim& S, int f) {
+__device__ inline void on_flow(Sim& S, Hot& H, int f) {
     if (S.fdraw[f] != 0) {                                          // SendPacket :297-358
-        Hdr& h = *S.h;
         uint32_t src = (uint32_t)S.fsrc[f];
         uint4 e;
-        e.x = ent_make(T_DATA, src, (uint32_t)S.fdst[f], 1u, 1u, (uint32_t)(h.now / 1000000000));
-        e.y = h.uid++;
+        e.x = ent_make(T_DATA, src, (uint32_t)S.fdst[f], 1u, 1u, (uint32_t)(H.now / 1000000000));
+        e.y = H.uid++;
         e.z = 0xffffffffu;
         e.w = 0;
-        link_send(S, S.L->E + (int)src, e);                         // access link
+        link_send(S, H, S.L->E + (int)src, e);                      // access link
     }
-    flow_next(S, f);                                                // StartSending / ScheduleNextTx
+    flow_next(S, H, f);                                             // StartSending / ScheduleNextTx
 }
 
-// returns 1 if a decision is pending (needs an action)
-__device__ inline int on_arrive(Sim& S, int l) {
-    Hdr& h = *S.h;
+// Returns 1 if a data decision needs an action (its entry/node/record in *pe/*pv/*pd).
+__device__ inline int on_arrive(Sim& S, Hot& H, int l, uint4* pe, int* pv, uint32_t* pd, double* prew,
+                                int32_t* pprev, bool fused) {
+    const Layout& L = *S.L;
     LinkState& k = S.ln[l];
-    uint32_t cap = S.rcap[l];
+    uint32_t cap = ring_cap(L, l);
     uint32_t hi = k.head;
-    uint4 e = S.ring[S.rofs[l] + hi];
+    uint4 e = S.ring[ring_off(L, l) + hi];
     k.head = (uint16_t)(hi + 1 == cap ? 0 : hi + 1);
     k.n_wire--;
+    relink(S, l);
     int v = S.ldst[l];
     uint32_t type = ent_type(e.x);
     if (type == T_DATA) {
         // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
         uint32_t dst = ent_dst(e.x);
-        uint32_t d = h.dec_count++;
+        uint32_t d = H.dec++;
         double reward = 0.0;
         int32_t prev = -1;
         if (!ent_fresh(e.x)) {
             prev = (int32_t)e.z;
-            reward = py_reward(h.now, e.w);                        // forwarder.py:360
-            S.c->reward_sum += reward;
+            reward = py_reward(H.now, e.w);                        // forwarder.py:360
+            H.c.reward_sum += reward;
         }
-        observe(S, v, dst);
-        S.c->decisions++;
+        observe(S, H, v, dst);
+        H.c.decisions++;
         if (dst == (uint32_t)v) {                                   // getGameOver
-            write_record(S, d, h.now, reward, e.y, prev, (uint32_t)v, dst, -1, PRISMA_ST_DESTINATION);
-            receive_counters(S, e.x, v);
+            write_record(S, H, d, reward, e.y, prev, (uint32_t)v, dst, -1, PRISMA_ST_DESTINATION);
+            receive_counters(L, H, e.x, v);
             return 0;
         }
-        write_record(S, d, h.now, reward, e.y, prev, (uint32_t)v, dst, -1, PRISMA_ST_PENDING);
-        h.pend = 1;
-        h.pend_link = (uint32_t)l;
-        h.pend_node = (uint32_t)v;
-        h.pend_dec = d;
-        h.pend_ent[0] = e.x; h.pend_ent[1] = e.y; h.pend_ent[2] = e.z; h.pend_ent[3] = e.w;
+        if (!fused) write_record(S, H, d, reward, e.y, prev, (uint32_t)v, dst, -1, PRISMA_ST_PENDING);
+        *pe = e; *pv = v; *pd = d; *prew = reward; *pprev = prev;
         return 1;
     }
     if (type == T_PING_FWD) {                                       // ping-forward-packet-manager.cc:94-156
-        float delay = (float)(ns_to_sec(h.now) - ((double)e.z * 0.001));
+        float delay = (float)(ns_to_sec(H.now) - ((double)e.z * 0.001));
         uint4 b;
         b.x = ent_make(T_PING_BACK, (uint32_t)v, ent_src(e.x), 0u, 0u, ent_aux(e.x));
         b.y = e.y;
         b.z = __float_as_uint(delay);
         b.w = 0;
-        if (!link_send(S, S.lrev[l], b)) S.c->ctrl_dropped++;
+        if (!link_send(S, H, S.lrev[l], b)) H.c.ctrl_dropped++;
     } else if (type == T_PING_BACK) {                               // ping-back-packet-manager.cc:120-144
         int lt = S.rowptr[v] + (int)ent_aux(e.x);
         PingMeta& m = S.pm[lt];
         int32_t idx = (int32_t)e.y;
         if (idx <= m.acked_last) {
-            fail(S, PRISMA_EBIT_ACKORDER);
+            fail(H, PRISMA_EBIT_ACKORDER);
         } else {
             if (idx > m.acked_last + 1 && m.first_hole < 0) m.first_hole = m.acked_last + 1;
             m.acked_last = idx;
         }
-        uint32_t MA = S.L->ma;
+        uint32_t MA = L.ma;
         uint32_t slot;
         if (m.win_n >= MA) {
             slot = m.win_head;
@@ -493,12 +563,12 @@ __device__ inline int on_arrive(Sim& S, int l) {
         }
         S.win[(uint32_t)lt * MA + slot] = __uint_as_float(e.z);
     }
-    receive_counters(S, e.x, v);
+    receive_counters(L, H, e.x, v);
     return 0;
 }
 
 // ---------------------------------------------------------------------------
-// replica (re)initialisation: all lanes
+// replica (re)initialisation: all lanes, operates on the LDS image
 // ---------------------------------------------------------------------------
 __device__ void init_replica(Sim& S, int lane, uint32_t episode) {
     const Layout& L = *S.L;
@@ -514,8 +584,11 @@ __device__ void init_replica(Sim& S, int lane, uint32_t episode) {
         philox4x32_10(c, L.seed_lo, S.gid);
         uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
         double U = (double)u53 * (1.0 / 9007199254740992.0);
-        S.ft[f] = sec_to_ns(0.0001 + U);                           // sim.cc:610-630
-        S.fseq[f] = (uint32_t)(L.N + f);
+        CKey key;
+        key.t = sec_to_ns(0.0001 + U);                             // sim.cc:610-630
+        key.seq = (uint32_t)(L.N + f);
+        key.code = (K_FLOW << 28) | (uint32_t)f;
+        S.fkey[f] = key;
         S.fdraw[f] = 0;
     }
     for (int l = lane; l < L.E; l += kWave) {
@@ -523,8 +596,9 @@ __device__ void init_replica(Sim& S, int lane, uint32_t episode) {
         S.pm[l].first_hole = -1;
     }
     for (int l = lane; l < L.L; l += kWave) {
-        LinkState& k = S.ln[l];
-        k.complete_t = 0;
+        CKey key;
+        key.t = INT64_MAX; key.seq = 0xffffffffu; key.code = 0xffffffffu;
+        S.lkey[l] = key;
     }
     if (lane == 0) {
         Hdr& h = *S.h;
@@ -543,40 +617,75 @@ __device__ void init_replica(Sim& S, int lane, uint32_t episode) {
 }
 
 // ---------------------------------------------------------------------------
-// wave-wide event selection
+// wave-wide event selection: per-lane min over owned candidate keys, then a
+// DPP reduction of the 64-bit time to lane 63; the (rare) same-ns ties are
+// resolved by a second reduction of seq over the tied lanes.
 // ---------------------------------------------------------------------------
-__device__ inline bool key_less(int64_t t, uint32_t s, int64_t bt, uint32_t bs) {
-    return t < bt || (t == bt && s < bs);
+template <int CTRL, int ROW_MASK>
+__device__ inline uint32_t dpp_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xf, false);
 }
 
-__device__ inline void select_event(const Sim& S, int lane, int64_t& bt, uint32_t& bs, uint32_t& bc) {
+template <int CTRL, int ROW_MASK>
+__device__ inline int64_t dpp_min_i64(int64_t v) {
+    uint32_t lo = dpp_u32<CTRL, ROW_MASK>((uint32_t)v);
+    uint32_t hi = dpp_u32<CTRL, ROW_MASK>((uint32_t)((uint64_t)v >> 32));
+    int64_t o = (int64_t)(((uint64_t)hi << 32) | lo);
+    return o < v ? o : v;
+}
+
+template <int CTRL, int ROW_MASK>
+__device__ inline uint32_t dpp_min_u32(uint32_t v) {
+    uint32_t o = dpp_u32<CTRL, ROW_MASK>(v);
+    return o < v ? o : v;
+}
+
+__device__ inline int64_t wave_min_i64(int64_t v) {
+    v = dpp_min_i64<0xB1, 0xF>(v);      // quad_perm [1,0,3,2]
+    v = dpp_min_i64<0x4E, 0xF>(v);      // quad_perm [2,3,0,1]
+    v = dpp_min_i64<0x141, 0xF>(v);     // row_half_mirror
+    v = dpp_min_i64<0x140, 0xF>(v);     // row_mirror
+    v = dpp_min_i64<0x142, 0xA>(v);     // row_bcast:15
+    v = dpp_min_i64<0x143, 0xC>(v);     // row_bcast:31
+    uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), 63);
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ inline uint32_t wave_min_u32(uint32_t v) {
+    v = dpp_min_u32<0xB1, 0xF>(v);
+    v = dpp_min_u32<0x4E, 0xF>(v);
+    v = dpp_min_u32<0x141, 0xF>(v);
+    v = dpp_min_u32<0x140, 0xF>(v);
+    v = dpp_min_u32<0x142, 0xA>(v);
+    v = dpp_min_u32<0x143, 0xC>(v);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+__device__ inline void select_event(const Sim& S, const Hot& H, int lane, int64_t& bt, uint32_t& bc) {
     const Layout& L = *S.L;
-    bt = INT64_MAX; bs = 0xffffffffu; bc = 0xffffffffu;
+    int64_t t = INT64_MAX;
+    uint32_t s = 0xffffffffu, c = 0xffffffffu;
     for (int f = lane; f < L.F; f += kWave) {
-        int64_t t = S.ft[f]; uint32_t s = S.fseq[f];
-        if (key_less(t, s, bt, bs)) { bt = t; bs = s; bc = (K_FLOW << 28) | (uint32_t)f; }
+        CKey k = S.fkey[f];
+        if (key_less(k.t, k.seq, t, s)) { t = k.t; s = k.seq; c = k.code; }
     }
     for (int l = lane; l < L.L; l += kWave) {
-        const LinkState& k = S.ln[l];
-        if (k.busy && key_less(k.complete_t, k.complete_seq, bt, bs)) {
-            bt = k.complete_t; bs = k.complete_seq; bc = (K_COMPLETE << 28) | (uint32_t)l;
-        }
-        if (k.n_wire) {
-            uint32_t w = (uint32_t)l * L.WCAP + ((uint32_t)k.head & (uint32_t)(L.WCAP - 1));
-            int64_t t = S.wt[w]; uint32_t s = S.wseq[w];
-            if (key_less(t, s, bt, bs)) { bt = t; bs = s; bc = (K_ARRIVE << 28) | (uint32_t)l; }
-        }
+        CKey k = S.lkey[l];
+        if (key_less(k.t, k.seq, t, s)) { t = k.t; s = k.seq; c = k.code; }
     }
-    if (lane == 0 && key_less(S.h->ping_t, S.h->ping_seq, bt, bs)) {
-        bt = S.h->ping_t; bs = S.h->ping_seq; bc = (K_PING << 28);
+    if (lane == 0 && key_less(H.ping_t, H.ping_seq, t, s)) { t = H.ping_t; s = H.ping_seq; c = K_PING << 28; }
+    const int64_t tmin = wave_min_i64(t);
+    uint64_t tied = __ballot(t == tmin);
+    int win;
+    if ((tied & (tied - 1)) == 0) {
+        win = __builtin_ctzll(tied);
+    } else {                                                        // same-ns events: ns-3 uid order
+        uint32_t smin = wave_min_u32(t == tmin ? s : 0xffffffffu);
+        win = __builtin_ctzll(__ballot(t == tmin && s == smin));
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        int64_t t2 = __shfl_xor(bt, off);
-        uint32_t s2 = __shfl_xor(bs, off);
-        uint32_t c2 = __shfl_xor(bc, off);
-        if (key_less(t2, s2, bt, bs)) { bt = t2; bs = s2; bc = c2; }
-    }
+    bt = tmin;
+    bc = (uint32_t)__builtin_amdgcn_readlane((int)c, win);
 }
 
 // ---------------------------------------------------------------------------
@@ -605,21 +714,6 @@ __device__ inline void stage_out(unsigned char* lds, const KParams& P, int r, in
 }
 
 __device__ inline void publish_counters(Sim& S, const KParams& P, int r, int lane) {
-    if (lane == 0) {
-        Hdr& h = *S.h;
-        prisma_counters_t& c = *S.c;
-        c.now_ns = h.now;
-        c.episode = h.episode;
-        c.ping_rounds = h.ping_rounds;
-        c.seq = h.seq;
-        c.uid = h.uid;
-        c.dec_count = h.dec_count;
-        c.error = h.error;
-        c.episode_over = h.over;
-        c.hops_total = h.hops_total;
-        c.events_total = h.events_total;
-    }
-    __syncthreads();
     const uint32_t* src = (const uint32_t*)S.c;
     uint32_t* dst = (uint32_t*)(P.cnt_out + r);
     if (lane < (int)(sizeof(prisma_counters_t) / 4)) dst[lane] = src[lane];
@@ -634,10 +728,15 @@ extern "C" __global__ void __launch_bounds__(64) prisma_reset_kernel(KParams P) 
     for (uint32_t i = (uint32_t)lane; i < L.topo_bytes / 16u; i += kWave) l4[i] = t4[i];
     Sim S;
     sim_bind(S, L, lds, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r);
-    if (lane == 0) { S.h->dec_count = 0; S.h->hops_total = 0; S.h->events_total = 0; }
+    if (lane == 0) { S.h->dec_count = 0; S.h->hops_total = 0; S.h->events_total = 0; S.h->hops_launch = 0; }
     init_replica(S, lane, P.episode);
-    publish_counters(S, P, r, lane);
+    if (lane == 0) {
+        Hot H;
+        hot_load(S, H);
+        hot_store(S, H);
+    }
     __syncthreads();
+    publish_counters(S, P, r, lane);
     stage_out(lds, P, r, lane);
 }
 
@@ -651,78 +750,91 @@ extern "C" __global__ void __launch_bounds__(64) prisma_step_kernel(KParams P) {
     sim_bind(S, L, lds, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r);
     const bool table_mode = (P.mode == 2);
     const uint32_t max_hops = (uint32_t)P.max_hops;
+    const uint32_t NN = (uint32_t)L.N;
+    Hot H;
+    hot_load(S, H);                                    // every lane holds a copy; lane 0 owns it
 
     if (lane == 0) {
-        Hdr& h = *S.h;
-        h.stop = 0;
-        h.hops_launch = 0;
-        if (h.pend && !h.over) {
+        H.stop = 0;
+        H.hops_launch = 0;
+        if (H.pend && !H.over) {
             if (table_mode) {
-                finish_decision(S, (int)S.table[h.pend_node * (uint32_t)L.N + ent_dst(h.pend_ent[0])]);
-                h.hops_launch++;
-                h.hops_total++;
+                finish_pending(S, H, (int)S.table[S.h->pend_node * NN + ent_dst(S.h->pend_ent[0])]);
+                H.hops_launch++;
+                H.hops_total++;
             } else if (P.actions) {
-                finish_decision(S, (int)P.actions[r]);
+                finish_pending(S, H, (int)P.actions[r]);
             } else {
-                h.stop = 1;                          // nothing to apply: re-emit the pending obs
+                H.stop = 1;                            // nothing to apply: re-emit the pending obs
             }
         }
-        if (h.over || (table_mode && h.hops_launch >= max_hops)) h.stop = 1;
+        if (H.over || (table_mode && H.hops_launch >= max_hops)) H.stop = 1;
     }
     __syncthreads();
-
+    uint32_t stop = (uint32_t)__builtin_amdgcn_readfirstlane((int)H.stop);
     uint32_t resets = 0;
-    while (!S.h->stop) {
+    while (!stop) {
         int64_t bt;
-        uint32_t bs, bc;
-        select_event(S, lane, bt, bs, bc);
-        if (bt >= L.t_end) {                         // Simulator::Stop(simTime) (sim.cc:703)
-            if (L.auto_reset && resets < 64u) {   // bounded: an empty scenario cannot spin forever
+        uint32_t bc;
+        select_event(S, H, lane, bt, bc);
+        if (bt >= L.t_end) {                           // Simulator::Stop(simTime) (sim.cc:703)
+            if (L.auto_reset && resets < 64u) {        // bounded: an empty scenario cannot spin forever
                 ++resets;
-                init_replica(S, lane, S.h->episode + 1u);
+                if (lane == 0) hot_store(S, H);
+                init_replica(S, lane, H.episode + 1u);
+                hot_load(S, H);
                 continue;
             }
-            if (lane == 0) { S.h->over = 1; S.h->stop = 1; }
-            __syncthreads();
+            if (lane == 0) { H.over = 1; H.stop = 1; }
             break;
         }
         if (lane == 0) {
-            Hdr& h = *S.h;
-            h.now = bt;
-            S.c->events++;
-            h.events_total++;
+            H.now = bt;
+            H.c.events++;
+            H.events_total++;
             const uint32_t kind = bc >> 28, id = bc & 0x0fffffffu;
-            int need = 0;
-            if (kind == K_ARRIVE) need = on_arrive(S, (int)id);
-            else if (kind == K_COMPLETE) on_complete(S, (int)id);
-            else if (kind == K_FLOW) on_flow(S, (int)id);
-            else on_ping_round(S);
-            if (need) {
-                if (table_mode) {
-                    finish_decision(S, (int)S.table[h.pend_node * (uint32_t)L.N + ent_dst(h.pend_ent[0])]);
-                    h.hops_launch++;
-                    h.hops_total++;
-                    if (h.hops_launch >= max_hops) h.stop = 1;
-                } else {
-                    h.stop = 1;
+            if (kind == K_ARRIVE) {
+                uint4 e; int v; uint32_t d; double rw; int32_t pv;
+                if (on_arrive(S, H, (int)id, &e, &v, &d, &rw, &pv, table_mode)) {
+                    if (table_mode) {
+                        apply_decision(S, H, e, v, d, (int)S.table[(uint32_t)v * NN + ent_dst(e.x)], true, rw, pv);
+                        H.hops_launch++;
+                        H.hops_total++;
+                        if (H.hops_launch >= max_hops) H.stop = 1;
+                    } else {
+                        Hdr& h = *S.h;
+                        h.pend_link = id; h.pend_node = (uint32_t)v; h.pend_dec = d;
+                        h.pend_ent[0] = e.x; h.pend_ent[1] = e.y; h.pend_ent[2] = e.z; h.pend_ent[3] = e.w;
+                        H.pend = 1;
+                        H.stop = 1;
+                    }
                 }
+            } else if (kind == K_COMPLETE) {
+                on_complete(S, H, (int)id);
+            } else if (kind == K_FLOW) {
+                on_flow(S, H, (int)id);
+            } else {
+                on_ping_round(S, H);
             }
-            if (h.error) { h.over = 1; h.stop = 1; }
+            if (H.error) { H.over = 1; H.stop = 1; }
         }
         __syncthreads();
+        stop = (uint32_t)__builtin_amdgcn_readfirstlane((int)H.stop);
     }
 
+    if (lane == 0) hot_store(S, H);
+    __syncthreads();
     const bool pending = S.h->pend && !S.h->over;
     if (P.mask_out && lane == 0) P.mask_out[r] = pending ? 1 : 0;
     if (P.node_out && lane == 0) P.node_out[r] = pending ? (int32_t)S.h->pend_node : -1;
     if (P.obs_out && lane < L.W) P.obs_out[(size_t)r * L.W + lane] = pending ? (int32_t)S.obs[lane] : 0;
     publish_counters(S, P, r, lane);
-    __syncthreads();
     stage_out(lds, P, r, lane);
 }
 
 // Gather records (replica[i], dec[i]) into a dense array: one lane per 4-byte
 // word, a wave per group of records (record rows are 48-64 B, so a wave
+// writes 1 KiB contiguous destination rows).
 // writes 1 KiB contiguous destination rows).
 extern "C" __global__ void __launch_bounds__(256) prisma_gather_kernel(
         const unsigned char* log, uint32_t log_cap, uint32_t rec_bytes, const int32_t* replica,
@@ -800,51 +912,42 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     memset(&L, 0, sizeof(L));
     const int Lk = E + N;
     L.N = N; L.E = E; L.L = Lk; L.F = F; L.max_deg = maxdeg;
-    L.W = (1 + maxdeg) + ((1 + maxdeg) & 1);
+    L.W = (1 + maxdeg + 3) & ~3;                    // obs width: multiple of 4 (16-B record rows)
     L.MA = (int)P->ma_size;
     L.data_size = P->packet_size + 30u;             // UDP 8 + IP 20 + PPP 2
     L.ping_size = 8u + 30u;
-    // per-link transmission / propagation (sim.cc:398-433)
-    std::vector<int64_t> txd(Lk), txp(Lk), prop(Lk);
-    std::vector<int32_t> ldst(Lk), lfrom(Lk);
-    std::vector<uint32_t> qmax(Lk);
+    // link constants (sim.cc:398-433): switch links share rate, delay and queue
+    L.sw_txd = sec_to_ns((double)L.data_size * 8 / (double)P->link_bps);
+    L.sw_txp = sec_to_ns((double)L.ping_size * 8 / (double)P->link_bps);
+    L.sw_prop = P->link_delay_ns;
+    L.qmax_bytes = P->max_buffer_bytes;
+    L.acc_qmax_pkts = 1000u;                        // "1000p" packet-mode access queue
+    std::vector<int64_t> acctx(N);
+    std::vector<int32_t> ldst(Lk);
     for (int u = 0; u < N; ++u)
-        for (int l = T->row_ptr[u]; l < T->row_ptr[u + 1]; ++l) { lfrom[l] = u; ldst[l] = T->link_dst[l]; }
-    for (int l = 0; l < E; ++l) {
-        txd[l] = sec_to_ns((double)L.data_size * 8 / (double)P->link_bps);
-        txp[l] = sec_to_ns((double)L.ping_size * 8 / (double)P->link_bps);
-        prop[l] = P->link_delay_ns;
-        qmax[l] = P->max_buffer_bytes;
-    }
+        for (int l = T->row_ptr[u]; l < T->row_ptr[u + 1]; ++l) ldst[l] = T->link_dst[l];
     for (int u = 0; u < N; ++u) {
-        int l = E + u;
         uint64_t bps = (uint64_t)1000000 * P->link_bps * (uint64_t)(T->row_ptr[u + 1] - T->row_ptr[u]);
-        txd[l] = sec_to_ns((double)L.data_size * 8 / (double)bps);
-        txp[l] = sec_to_ns((double)L.ping_size * 8 / (double)bps);
-        prop[l] = 0;
-        ldst[l] = u; lfrom[l] = -1;
-        qmax[l] = 0x80000000u | 1000u;              // "1000p" packet-mode queue
+        acctx[u] = sec_to_ns((double)L.data_size * 8 / (double)bps);
+        ldst[E + u] = u;
     }
     // wire capacity: packets whose transmission ended within the last
     // propagation delay, plus the one being transmitted
-    int64_t txmin = txp[0];
-    for (int l = 0; l < E; ++l) txmin = txp[l] < txmin ? txp[l] : txmin;
-    if (txmin < 1) return set_err(PRISMA_ERR_CONFIG, "link too fast for the wire model");
-    uint32_t wire = (uint32_t)(P->link_delay_ns / txmin) + 2u;
+    if (L.sw_txp < 1) return set_err(PRISMA_ERR_CONFIG, "link too fast for the wire model");
+    uint32_t wire = (uint32_t)(P->link_delay_ns / L.sw_txp) + 2u;
     L.WCAP = (int)next_pow2(wire < 2 ? 2 : wire);
     if (L.WCAP > 64) return set_err(PRISMA_ERR_CONFIG, "propagation delay too long for the wire model");
     // ring capacity: full byte-limited FIFO of data + the control packets that
     // can be queued at once (<= 2 pings per round over the FIFO's drain time)
-    double drain_s = (double)P->max_buffer_bytes * 8.0 / (double)P->link_bps + (double)txd[0] * 1e-9;
+    double drain_s = (double)P->max_buffer_bytes * 8.0 / (double)P->link_bps + (double)L.sw_txd * 1e-9;
     double span = 2.0 * drain_s + 2.0 * (double)P->link_delay_ns * 1e-9;
     uint32_t ctrl = 2u * ((uint32_t)(span / (double)P->ping_interval_s) + 3u);
     uint32_t qs = P->max_buffer_bytes / L.data_size + ctrl + (uint32_t)L.WCAP;
     qs = (qs + (uint32_t)L.WCAP - 1) / (uint32_t)L.WCAP * (uint32_t)L.WCAP;
-    uint32_t qa = (uint32_t)(L.WCAP < 8 ? 8 : L.WCAP);
     if (qs > 65535u) return set_err(PRISMA_ERR_CONFIG, "queue too deep");
-    std::vector<uint32_t> rofs(Lk), rcap(Lk);
-    uint32_t tot = 0;
-    for (int l = 0; l < Lk; ++l) { rcap[l] = l < E ? qs : qa; rofs[l] = tot; tot += rcap[l]; }
+    L.qcap_s = qs;
+    L.qcap_a = (uint32_t)(L.WCAP < 8 ? 8 : L.WCAP);
+    uint32_t tot = (uint32_t)E * L.qcap_s + (uint32_t)N * L.qcap_a;
 
     // topology image
     uint32_t o = 0;
@@ -852,13 +955,7 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.t_rowptr = take(4u * (N + 1));
     L.t_ldst = take(4u * Lk);
     L.t_lrev = take(4u * E);
-    L.t_lfrom = take(4u * Lk);
-    L.t_txd = take(8u * Lk);
-    L.t_txp = take(8u * Lk);
-    L.t_prop = take(8u * Lk);
-    L.t_rofs = take(4u * Lk);
-    L.t_rcap = take(4u * Lk);
-    L.t_qmax = take(4u * Lk);
+    L.t_acctx = take(8u * N);
     L.t_fsrc = take(4u * F);
     L.t_fdst = take(4u * F);
     L.t_fmean = take(8u * F);
@@ -869,13 +966,7 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     memcpy(&topo[L.t_rowptr], T->row_ptr, 4u * (N + 1));
     memcpy(&topo[L.t_ldst], ldst.data(), 4u * Lk);
     memcpy(&topo[L.t_lrev], T->link_rev, 4u * E);
-    memcpy(&topo[L.t_lfrom], lfrom.data(), 4u * Lk);
-    memcpy(&topo[L.t_txd], txd.data(), 8u * Lk);
-    memcpy(&topo[L.t_txp], txp.data(), 8u * Lk);
-    memcpy(&topo[L.t_prop], prop.data(), 8u * Lk);
-    memcpy(&topo[L.t_rofs], rofs.data(), 4u * Lk);
-    memcpy(&topo[L.t_rcap], rcap.data(), 4u * Lk);
-    memcpy(&topo[L.t_qmax], qmax.data(), 4u * Lk);
+    memcpy(&topo[L.t_acctx], acctx.data(), 8u * N);
     memcpy(&topo[L.t_fsrc], T->flow_src, 4u * F);
     memcpy(&topo[L.t_fdst], T->flow_dst, 4u * F);
     std::vector<double> fmean(F);
@@ -888,9 +979,9 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.s_hdr = take(sizeof(Hdr));
     L.s_cnt = take(sizeof(prisma_counters_t));
     L.s_obs = take(4u * L.W);
-    L.s_ft = take(8u * F);
-    L.s_fseq = take(4u * F);
+    L.s_fkey = take(16u * F);
     L.s_fdraw = take(4u * F);
+    L.s_lkey = take(16u * Lk);
     L.s_link = take(sizeof(LinkState) * Lk);
     L.s_wt = take(8u * Lk * L.WCAP);
     L.s_wseq = take(4u * Lk * L.WCAP);

@@ -10,8 +10,8 @@ EBIT_RING, EBIT_WIRE, EBIT_ACKORDER, EBIT_TIME = 1, 2, 4, 8
 
 def record_dtype(obs_width: int) -> np.dtype:
     """prisma_record_t with obs_width observation words (32 + 4*W bytes)."""
-    if obs_width % 2:
-        raise ValueError("obs_width must be even")
+    if obs_width % 4:
+        raise ValueError("obs_width must be a multiple of 4")
     return np.dtype([
         ("t_ns", "<i8"), ("reward", "<f8"), ("uid", "<u4"), ("prev", "<i4"),
         ("node", "<u2"), ("dst", "<u2"), ("action", "i1"), ("status", "u1"),

@@ -142,7 +142,7 @@ class Topology:
     @property
     def obs_width(self) -> int:
         w = 1 + self.max_deg
-        return w + (w & 1)
+        return (w + 3) & ~3
 
     def neighbors(self, u: int) -> List[int]:
         return [int(x) for x in self.link_dst[self.row_ptr[u]:self.row_ptr[u + 1]]]
