@@ -76,7 +76,10 @@ struct Layout {
     // topology image (LDS offset 0)
     uint32_t t_rowptr, t_ldst, t_lrev, t_acctx, t_fsrc, t_fdst, t_fmean, t_table;
     // state image (LDS offset topo_bytes)
-    uint32_t s_hdr, s_cnt, s_obs, s_fkey, s_fdraw, s_lkey, s_link, s_wt, s_wseq, s_ring, s_win, s_pmeta;
+    uint32_t s_hdr, s_cnt, s_obs, s_wt, s_wseq, s_ring, s_win;
+    uint32_t lds_state_bytes;    // LDS part of the image (bytes [0, lds_state_bytes))
+    uint32_t s_regs;             // register part: 4 x [64*FS] + 14 x [64*LS] u32 arrays
+    int32_t  FS, LS;             // flow / link register slots per lane
     // link constants (identical on every switch link: sim.cc:414-433)
     int64_t  sw_txd, sw_txp, sw_prop;
     uint32_t qcap_s, qcap_a, qmax_bytes, acc_qmax_pkts;

@@ -1,0 +1,91 @@
+// numerics.h — scalar building blocks shared by host sizing code and the
+// gfx950 kernels.  Every expression here is evaluated with the same IEEE-754
+// operation sequence on host and device (compile with -ffp-contract=off), so
+// results are bit-identical to the CPU oracle's independent restatement.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// ---------------------------------------------------------------------------
+// numeric building blocks (device + host, identical IEEE sequences)
+// ---------------------------------------------------------------------------
+__host__ __device__ inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
+    uint32_t c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
+        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
+        c1 = (uint32_t)p1;
+        c3 = (uint32_t)p0;
+        c0 = n0;
+        c2 = n2;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    c[0] = c0; c[1] = c1; c[2] = c2; c[3] = c3;
+}
+
+// ln(x) for x > 0 normal: range reduction to [sqrt(1/2), sqrt(2)] and the
+// atanh series; + - * / only.
+__host__ __device__ inline double det_log(double x) {
+    uint64_t bits = __builtin_bit_cast(uint64_t, x);
+    int e = (int)((bits >> 52) & 0x7ff) - 1023;
+    double m = __builtin_bit_cast(double, (bits & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL);
+    if (m > 1.4142135623730951) { m = m * 0.5; e += 1; }
+    double f = m - 1.0;
+    double s = f / (2.0 + f);
+    double z = s * s;
+    double p = 2.0 / 19.0;
+    p = p * z + 2.0 / 17.0;
+    p = p * z + 2.0 / 15.0;
+    p = p * z + 2.0 / 13.0;
+    p = p * z + 2.0 / 11.0;
+    p = p * z + 2.0 / 9.0;
+    p = p * z + 2.0 / 7.0;
+    p = p * z + 2.0 / 5.0;
+    p = p * z + 2.0 / 3.0;
+    double logm = 2.0 * s + s * (z * p);
+    double de = (double)e;
+    return de * 6.93147180369123816490e-01 + (de * 1.90821492927058770002e-10 + logm);
+}
+
+// ns-3 Seconds(double) -> int64 ns (round to nearest)
+__host__ __device__ inline int64_t sec_to_ns(double s) { return (int64_t)(s * 1e9 + 0.5); }
+// ns-3 Time::GetSeconds()
+__host__ __device__ inline double ns_to_sec(int64_t t) { return (double)t / 1e9; }
+
+// microseconds of std::to_string(GetSeconds()) (%f, ties-to-even on the
+// exact binary value) as Python reads them back (packet-manager.cc:127-128).
+__host__ __device__ inline uint64_t py_micros(int64_t t) {
+    uint64_t u = (uint64_t)(t / 1000);
+    int64_t r = t - (int64_t)u * 1000;
+    if (r != 500) return r < 500 ? u : u + 1;
+    double x = ns_to_sec(t);
+    uint64_t b = __builtin_bit_cast(uint64_t, x);
+    int ex = (int)((b >> 52) & 0x7ff);
+    uint64_t mant = (b & 0x000fffffffffffffULL) | (ex ? 0x0010000000000000ULL : 0);
+    if (!ex) ex = 1;
+    int sh = 1075 - ex;                      // x = mant * 2^-sh, sh > 0 here
+    // lhs = mant * 2e6 (< 2^75), rhs = (2u+1) << sh, compared as 128-bit
+    const uint64_t k = 2000000ull;
+    uint64_t lo = mant * k;
+#ifdef __HIP_DEVICE_COMPILE__
+    uint64_t hi = __umul64hi(mant, k);
+#else
+    uint64_t hi = (uint64_t)(((unsigned __int128)mant * k) >> 64);
+#endif
+    uint64_t v = 2 * u + 1, rhi, rlo;
+    if (sh >= 64) { rhi = v << (sh - 64); rlo = 0; }
+    else if (sh == 0) { rhi = 0; rlo = v; }
+    else { rhi = v >> (64 - sh); rlo = v << sh; }
+    if (hi != rhi) return hi > rhi ? u + 1 : u;
+    if (lo != rlo) return lo > rlo ? u + 1 : u;
+    return (u & 1) ? u + 1 : u;
+}
+
+__host__ __device__ inline double py_reward(int64_t t_now, uint32_t us_prev) {
+    return (double)py_micros(t_now) / 1e6 - (double)us_prev / 1e6;
+}
+

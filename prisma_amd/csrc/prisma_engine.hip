@@ -1,24 +1,25 @@
 // prisma_engine.hip — MI355X (gfx950) packet-hop engine behind include/prisma.h.
 //
-// Design (DESIGN.md): one 64-lane wavefront (= one workgroup) owns one
-// topology replica.  At launch the replica's state image is staged from HBM
-// into LDS with 16-byte coalesced loads; the wavefront then runs the
-// replica's discrete-event loop out of LDS:
-//   * next event = wave-wide min over (time_ns, seq) of every pending
-//     candidate — flow injections, link tx-completions, wire heads and the
-//     ping round — each lane scanning the candidates it owns, then a
-//     64-lane shuffle reduction (the ns-3 MapScheduler order);
-//   * the selected handler runs on lane 0 against LDS (FIFO push/pop in
-//     per-link rings, drop-on-overflow, link-delay accumulation, the
-//     Q-routing reward of forwarder.py:360);
-//   * each data notification appends one decision record to the replica's
-//     HBM transition log.
-// At exit the image is written back to HBM.  Results are bit-identical to
-// the CPU oracle (oracle/), which restates the reference ns-3 semantics.
+// Design (DESIGN.md §5): one 64-lane wavefront (= one workgroup) owns one
+// topology replica of PRISMA's ns-3 scenario and runs its discrete-event
+// loop for a whole launch.
+//   * Link and flow state is lane-distributed in VGPRs: link l lives in lane
+//     l % 64, register slot l / 64 (likewise flows).  Every lane keeps the
+//     next-event key (time, seq) of the sources it owns, so choosing the next
+//     event is a register-only per-lane min plus a DPP wave reduction (the
+//     ns-3 MapScheduler (time, uid) order) — no LDS, no barrier.
+//   * The selected handler runs as uniform code on all lanes: scalars live in
+//     SGPRs, a link's fields are read with v_readlane and written back with
+//     v_writelane into the owning lane.
+//   * Packet FIFOs (per-link rings of 16-B entries), wire arrival times and the
+//     ping windows live in LDS; the replica image is staged HBM -> LDS/VGPR at
+//     launch and written back at exit (16-B coalesced).
+//   * Every data notification appends a 32+4W-byte decision record to the
+//     replica's HBM log with one coalesced wave store.
+// Results are bit-identical to the CPU oracle (oracle/), the independent
+// restatement of the reference ns-3 semantics.
 //
 // Compile: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -fPIC -shared
-// (-ffp-contract=off keeps every double/float expression identical to the
-// oracle's; the reference quantities involved are cited where computed).
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
@@ -31,96 +32,14 @@
 
 #include "../../include/prisma.h"
 #include "engine_layout.h"
+#include "numerics.h"
 
 using namespace prisma;
 
 #define HIP_OK(x) ((x) == hipSuccess)
 
 // ---------------------------------------------------------------------------
-// numeric building blocks (device + host, identical IEEE sequences)
-// ---------------------------------------------------------------------------
-__host__ __device__ inline void philox4x32_10(uint32_t c[4], uint32_t k0, uint32_t k1) {
-    uint32_t c0 = c[0], c1 = c[1], c2 = c[2], c3 = c[3];
-#pragma unroll
-    for (int r = 0; r < 10; ++r) {
-        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
-        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
-        uint32_t n0 = (uint32_t)(p1 >> 32) ^ c1 ^ k0;
-        uint32_t n2 = (uint32_t)(p0 >> 32) ^ c3 ^ k1;
-        c1 = (uint32_t)p1;
-        c3 = (uint32_t)p0;
-        c0 = n0;
-        c2 = n2;
-        k0 += 0x9E3779B9u;
-        k1 += 0xBB67AE85u;
-    }
-    c[0] = c0; c[1] = c1; c[2] = c2; c[3] = c3;
-}
-
-// ln(x) for x > 0 normal: range reduction to [sqrt(1/2), sqrt(2)] and the
-// atanh series; + - * / only.
-__host__ __device__ inline double det_log(double x) {
-    uint64_t bits = __builtin_bit_cast(uint64_t, x);
-    int e = (int)((bits >> 52) & 0x7ff) - 1023;
-    double m = __builtin_bit_cast(double, (bits & 0x000fffffffffffffULL) | 0x3ff0000000000000ULL);
-    if (m > 1.4142135623730951) { m = m * 0.5; e += 1; }
-    double f = m - 1.0;
-    double s = f / (2.0 + f);
-    double z = s * s;
-    double p = 2.0 / 19.0;
-    p = p * z + 2.0 / 17.0;
-    p = p * z + 2.0 / 15.0;
-    p = p * z + 2.0 / 13.0;
-    p = p * z + 2.0 / 11.0;
-    p = p * z + 2.0 / 9.0;
-    p = p * z + 2.0 / 7.0;
-    p = p * z + 2.0 / 5.0;
-    p = p * z + 2.0 / 3.0;
-    double logm = 2.0 * s + s * (z * p);
-    double de = (double)e;
-    return de * 6.93147180369123816490e-01 + (de * 1.90821492927058770002e-10 + logm);
-}
-
-// ns-3 Seconds(double) -> int64 ns (round to nearest)
-__host__ __device__ inline int64_t sec_to_ns(double s) { return (int64_t)(s * 1e9 + 0.5); }
-// ns-3 Time::GetSeconds()
-__host__ __device__ inline double ns_to_sec(int64_t t) { return (double)t / 1e9; }
-
-// microseconds of std::to_string(GetSeconds()) (%f, ties-to-even on the
-// exact binary value) as Python reads them back (packet-manager.cc:127-128).
-__host__ __device__ inline uint64_t py_micros(int64_t t) {
-    uint64_t u = (uint64_t)(t / 1000);
-    int64_t r = t - (int64_t)u * 1000;
-    if (r != 500) return r < 500 ? u : u + 1;
-    double x = ns_to_sec(t);
-    uint64_t b = __builtin_bit_cast(uint64_t, x);
-    int ex = (int)((b >> 52) & 0x7ff);
-    uint64_t mant = (b & 0x000fffffffffffffULL) | (ex ? 0x0010000000000000ULL : 0);
-    if (!ex) ex = 1;
-    int sh = 1075 - ex;                      // x = mant * 2^-sh, sh > 0 here
-    // lhs = mant * 2e6 (< 2^75), rhs = (2u+1) << sh, compared as 128-bit
-    const uint64_t k = 2000000ull;
-    uint64_t lo = mant * k;
-#ifdef __HIP_DEVICE_COMPILE__
-    uint64_t hi = __umul64hi(mant, k);
-#else
-    uint64_t hi = (uint64_t)(((unsigned __int128)mant * k) >> 64);
-#endif
-    uint64_t v = 2 * u + 1, rhi, rlo;
-    if (sh >= 64) { rhi = v << (sh - 64); rlo = 0; }
-    else if (sh == 0) { rhi = 0; rlo = v; }
-    else { rhi = v >> (64 - sh); rlo = v << sh; }
-    if (hi != rhi) return hi > rhi ? u + 1 : u;
-    if (lo != rlo) return lo > rlo ? u + 1 : u;
-    return (u & 1) ? u + 1 : u;
-}
-
-__host__ __device__ inline double py_reward(int64_t t_now, uint32_t us_prev) {
-    return (double)py_micros(t_now) / 1e6 - (double)us_prev / 1e6;
-}
-
-// ---------------------------------------------------------------------------
-// device-side replica view
+// kernel parameters
 // ---------------------------------------------------------------------------
 struct KParams {
     Layout lay;
@@ -139,59 +58,118 @@ struct KParams {
     int32_t mode;                // 0 reset, 1 external step, 2 table run
 };
 
-// candidate key of one event source: 16 bytes, read with one ds_read_b128
-struct __attribute__((aligned(16))) CKey {
-    int64_t  t;
-    uint32_t seq;
-    uint32_t code;               // kind << 28 | index
+// ---------------------------------------------------------------------------
+// cross-lane helpers
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t lane) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+// write one lane of a VGPR (v_cmp + v_cndmask; there is no writelane builtin)
+__device__ __forceinline__ uint32_t wrl(uint32_t old, uint32_t v, uint32_t lane) {
+    return threadIdx.x == lane ? v : old;
+}
+__device__ __forceinline__ int64_t mk64(uint32_t lo, uint32_t hi) { return (int64_t)(((uint64_t)hi << 32) | lo); }
+__device__ __forceinline__ uint32_t lo32(int64_t v) { return (uint32_t)(uint64_t)v; }
+__device__ __forceinline__ uint32_t hi32(int64_t v) { return (uint32_t)((uint64_t)v >> 32); }
+
+// A lane-distributed u32 array of 64*S elements: element i lives in lane
+// i % 64, register slot i / 64.  get/set take a wave-uniform index.
+template <int S>
+struct LA {
+    uint32_t v[S];
+    __device__ __forceinline__ uint32_t get(uint32_t i) const {
+        const uint32_t slot = i >> 6, owner = i & 63u;
+        uint32_t r = 0;
+#pragma unroll
+        for (int j = 0; j < S; ++j)
+            if ((uint32_t)j == slot) r = rdl(v[j], owner);
+        return r;
+    }
+    __device__ __forceinline__ void set(uint32_t i, uint32_t x) {
+        const uint32_t slot = i >> 6, owner = i & 63u;
+#pragma unroll
+        for (int j = 0; j < S; ++j)
+            if ((uint32_t)j == slot) v[j] = wrl(v[j], x, owner);
+    }
+    __device__ __forceinline__ void load(const uint32_t* img, int lane) {
+#pragma unroll
+        for (int j = 0; j < S; ++j) v[j] = img[lane + 64 * j];
+    }
+    __device__ __forceinline__ void store(uint32_t* img, int lane) const {
+#pragma unroll
+        for (int j = 0; j < S; ++j) img[lane + 64 * j] = v[j];
+    }
 };
 
-// Lane-0 scalar state kept in registers for the whole event loop; it is
-// loaded from / stored to the Hdr + counters of the LDS image at the loop
-// boundaries only.
+// register-resident replica state (image order: the fields below, each a
+// [64*S] u32 array)
+template <int FS, int LS>
+struct Regs {
+    LA<FS> fk_lo, fk_hi, fk_seq, f_draw;         // flow next event (time, seq) + draw index
+    LA<LS> lk_lo, lk_hi, lk_seq, lk_kind;        // link next event key: kind 0 none / K_COMPLETE / K_ARRIVE
+    LA<LS> cp_lo, cp_hi, cp_seq;                 // tx completion event (valid while busy)
+    LA<LS> p0, p1, p2, qb;                       // head|txp<<16, tail|n_wire<<16, n_queue|busy<<16, queued bytes
+    LA<LS> pm_ack, pm_hole, pm_win;              // ping: last ack, first hole, win_n|win_head<<16
+    static constexpr int NF = 4, NL = 14;
+};
+
+template <int FS, int LS>
+__device__ __forceinline__ void regs_io(Regs<FS, LS>& R, uint32_t* img, int lane, bool store) {
+    uint32_t* fb = img;
+    uint32_t* lb = img + 4 * 64 * FS;
+#define RIO_F(fld, a) if (store) R.fld.store(fb + (a) * 64 * FS, lane); else R.fld.load(fb + (a) * 64 * FS, lane);
+#define RIO_L(fld, a) if (store) R.fld.store(lb + (a) * 64 * LS, lane); else R.fld.load(lb + (a) * 64 * LS, lane);
+    RIO_F(fk_lo, 0) RIO_F(fk_hi, 1) RIO_F(fk_seq, 2) RIO_F(f_draw, 3)
+    RIO_L(lk_lo, 0) RIO_L(lk_hi, 1) RIO_L(lk_seq, 2) RIO_L(lk_kind, 3) RIO_L(cp_lo, 4) RIO_L(cp_hi, 5)
+    RIO_L(cp_seq, 6) RIO_L(p0, 7) RIO_L(p1, 8) RIO_L(p2, 9) RIO_L(qb, 10) RIO_L(pm_ack, 11)
+    RIO_L(pm_hole, 12) RIO_L(pm_win, 13)
+#undef RIO_F
+#undef RIO_L
+}
+
+// wave-uniform scalar state ("SGPR state"): clock, counters, event sources
 struct Hot {
     int64_t  now, ping_t;
     uint32_t ping_seq, seq, uid, dec, ping_rounds, episode;
     uint32_t pend, over, error, stop, hops_launch;
     uint64_t hops_total, events_total;
-    prisma_counters_t c;
 };
 
+// counters live in LDS and are updated by lane 0 only (keeps them out of SGPRs)
+#define CNT(S_, field_) if ((S_).lane == 0) (S_).c->field_
+
+// LDS views of one replica
 struct Sim {
     const Layout* L;
-    unsigned char* base;         // LDS base
+    unsigned char* base;
     Hdr* h;
     prisma_counters_t* c;
     uint32_t* obs;
-    CKey* fkey; uint32_t* fdraw;
-    CKey* lkey; LinkState* ln;
     int64_t* wt; uint32_t* wseq;
     uint4* ring;
-    float* win; PingMeta* pm;
+    float* win;
     const int32_t* rowptr; const int32_t* ldst; const int32_t* lrev;
     const int64_t* acctx;
     const int32_t* fsrc; const int32_t* fdst; const double* fmean;
     const uint8_t* table;
-    unsigned char* logrep;       // this replica's log ring (HBM)
-    uint32_t gid;                // global replica id
+    unsigned char* logrep;
+    uint32_t gid;
+    int lane;
 };
 
-__device__ inline void sim_bind(Sim& S, const Layout& L, unsigned char* lds, unsigned char* logrep, uint32_t gid) {
+__device__ inline void sim_bind(Sim& S, const Layout& L, unsigned char* lds, unsigned char* logrep, uint32_t gid,
+                                int lane) {
     S.L = &L;
     S.base = lds;
     unsigned char* st = lds + L.topo_bytes;
     S.h = (Hdr*)(st + L.s_hdr);
     S.c = (prisma_counters_t*)(st + L.s_cnt);
     S.obs = (uint32_t*)(st + L.s_obs);
-    S.fkey = (CKey*)(st + L.s_fkey);
-    S.fdraw = (uint32_t*)(st + L.s_fdraw);
-    S.lkey = (CKey*)(st + L.s_lkey);
-    S.ln = (LinkState*)(st + L.s_link);
     S.wt = (int64_t*)(st + L.s_wt);
     S.wseq = (uint32_t*)(st + L.s_wseq);
     S.ring = (uint4*)(st + L.s_ring);
     S.win = (float*)(st + L.s_win);
-    S.pm = (PingMeta*)(st + L.s_pmeta);
     S.rowptr = (const int32_t*)(lds + L.t_rowptr);
     S.ldst = (const int32_t*)(lds + L.t_ldst);
     S.lrev = (const int32_t*)(lds + L.t_lrev);
@@ -202,142 +180,200 @@ __device__ inline void sim_bind(Sim& S, const Layout& L, unsigned char* lds, uns
     S.table = (const uint8_t*)(lds + L.t_table);
     S.logrep = logrep;
     S.gid = gid;
+    S.lane = lane;
+}
+
+// uniform LDS reads (every lane reads the same address: broadcast, no conflict)
+__device__ __forceinline__ uint32_t u_ld32(const uint32_t* p) { return rfl(*p); }
+__device__ __forceinline__ int32_t u_ldi(const int32_t* p) { return (int32_t)rfl((uint32_t)*p); }
+__device__ __forceinline__ int64_t u_ld64(const int64_t* p) {
+    int64_t v = *p;
+    return mk64(rfl(lo32(v)), rfl(hi32(v)));
+}
+__device__ __forceinline__ uint4 u_ld128(const uint4* p) {
+    uint4 v = *p;
+    return make_uint4(rfl(v.x), rfl(v.y), rfl(v.z), rfl(v.w));
+}
+__device__ __forceinline__ double u_ldd(const double* p) {
+    double v = *p;
+    uint64_t b = __double_as_longlong(v);
+    return __longlong_as_double((long long)(((uint64_t)rfl((uint32_t)(b >> 32)) << 32) | rfl((uint32_t)b)));
 }
 
 __device__ inline void hot_load(const Sim& S, Hot& H) {
     const Hdr& h = *S.h;
-    H.now = h.now; H.ping_t = h.ping_t; H.ping_seq = h.ping_seq; H.seq = h.seq; H.uid = h.uid;
-    H.dec = h.dec_count; H.ping_rounds = h.ping_rounds; H.episode = h.episode; H.pend = h.pend;
-    H.over = h.over; H.error = h.error; H.stop = h.stop; H.hops_launch = h.hops_launch;
-    H.hops_total = h.hops_total; H.events_total = h.events_total;
-    H.c = *S.c;
+    H.now = u_ld64(&h.now); H.ping_t = u_ld64(&h.ping_t);
+    H.ping_seq = u_ld32(&h.ping_seq); H.seq = u_ld32(&h.seq); H.uid = u_ld32(&h.uid);
+    H.dec = u_ld32(&h.dec_count); H.ping_rounds = u_ld32(&h.ping_rounds); H.episode = u_ld32(&h.episode);
+    H.pend = u_ld32(&h.pend); H.over = u_ld32(&h.over); H.error = u_ld32(&h.error);
+    H.stop = u_ld32(&h.stop); H.hops_launch = u_ld32(&h.hops_launch);
+    H.hops_total = (uint64_t)u_ld64((const int64_t*)&h.hops_total);
+    H.events_total = (uint64_t)u_ld64((const int64_t*)&h.events_total);
 }
 
 __device__ inline void hot_store(Sim& S, const Hot& H) {
-    Hdr& h = *S.h;
-    h.now = H.now; h.ping_t = H.ping_t; h.ping_seq = H.ping_seq; h.seq = H.seq; h.uid = H.uid;
-    h.dec_count = H.dec; h.ping_rounds = H.ping_rounds; h.episode = H.episode; h.pend = H.pend;
-    h.over = H.over; h.error = H.error; h.stop = H.stop; h.hops_launch = H.hops_launch;
-    h.hops_total = H.hops_total; h.events_total = H.events_total;
-    prisma_counters_t c = H.c;
-    c.now_ns = H.now; c.episode = H.episode; c.ping_rounds = H.ping_rounds; c.seq = H.seq; c.uid = H.uid;
-    c.dec_count = H.dec; c.error = H.error; c.episode_over = H.over;
-    c.hops_total = H.hops_total; c.events_total = H.events_total;
-    *S.c = c;
+    if (S.lane == 0) {
+        Hdr& h = *S.h;
+        h.now = H.now; h.ping_t = H.ping_t; h.ping_seq = H.ping_seq; h.seq = H.seq; h.uid = H.uid;
+        h.dec_count = H.dec; h.ping_rounds = H.ping_rounds; h.episode = H.episode; h.pend = H.pend;
+        h.over = H.over; h.error = H.error; h.stop = H.stop; h.hops_launch = H.hops_launch;
+        h.hops_total = H.hops_total; h.events_total = H.events_total;
+        prisma_counters_t& c = *S.c;
+        c.now_ns = H.now; c.episode = H.episode; c.ping_rounds = H.ping_rounds; c.seq = H.seq; c.uid = H.uid;
+        c.dec_count = H.dec; c.error = H.error; c.episode_over = H.over;
+        c.hops_total = H.hops_total; c.events_total = H.events_total;
+    }
 }
 
-__device__ inline void fail(Hot& H, uint32_t bit) {
+__device__ __forceinline__ void fail(Hot& H, uint32_t bit) {
     H.error |= bit;
     H.over = 1;
     H.stop = 1;
 }
 
-__device__ inline bool key_less(int64_t t, uint32_t s, int64_t bt, uint32_t bs) {
+__device__ __forceinline__ bool key_less(int64_t t, uint32_t s, int64_t bt, uint32_t bs) {
     return t < bt || (t == bt && s < bs);
 }
 
-// ---- link FIFO / transmitter (point-to-point-net-device.cc:273-336, 595-666)
-__device__ inline uint32_t ent_size(const Layout& L, uint32_t x) {
+__device__ __forceinline__ uint32_t ent_size(const Layout& L, uint32_t x) {
     return ent_type(x) == T_DATA ? L.data_size : L.ping_size;
 }
-__device__ inline uint32_t ring_off(const Layout& L, int l) {
-    return l < L.E ? (uint32_t)l * L.qcap_s : (uint32_t)L.E * L.qcap_s + (uint32_t)(l - L.E) * L.qcap_a;
+__device__ __forceinline__ uint32_t ring_off(const Layout& L, uint32_t l) {
+    return l < (uint32_t)L.E ? l * L.qcap_s : (uint32_t)L.E * L.qcap_s + (l - (uint32_t)L.E) * L.qcap_a;
 }
-__device__ inline uint32_t ring_cap(const Layout& L, int l) { return l < L.E ? L.qcap_s : L.qcap_a; }
+__device__ __forceinline__ uint32_t ring_cap(const Layout& L, uint32_t l) { return l < (uint32_t)L.E ? L.qcap_s : L.qcap_a; }
 
-// recompute the candidate key of link l: next tx completion or wire head
-__device__ inline void relink(Sim& S, int l) {
-    const LinkState& k = S.ln[l];
-    CKey key;
-    key.t = INT64_MAX; key.seq = 0xffffffffu; key.code = 0xffffffffu;
-    if (k.busy) { key.t = k.complete_t; key.seq = k.complete_seq; key.code = (K_COMPLETE << 28) | (uint32_t)l; }
+// one link's fields as uniform scalars
+struct LinkV {
+    uint32_t head, txp, tail, n_wire, n_queue, busy, qb;
+    int64_t cp_t;
+    uint32_t cp_seq;
+};
+
+template <int FS, int LS>
+__device__ __forceinline__ LinkV link_get(const Regs<FS, LS>& R, uint32_t l) {
+    LinkV k;
+    uint32_t a = R.p0.get(l), b = R.p1.get(l), c = R.p2.get(l);
+    k.head = a & 0xffffu; k.txp = a >> 16;
+    k.tail = b & 0xffffu; k.n_wire = b >> 16;
+    k.n_queue = c & 0xffffu; k.busy = c >> 16;
+    k.qb = R.qb.get(l);
+    k.cp_t = mk64(R.cp_lo.get(l), R.cp_hi.get(l));
+    k.cp_seq = R.cp_seq.get(l);
+    return k;
+}
+
+// write back a link's fields and recompute its candidate key
+template <int FS, int LS>
+__device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, uint32_t l, const LinkV& k) {
+    R.p0.set(l, k.head | (k.txp << 16));
+    R.p1.set(l, k.tail | (k.n_wire << 16));
+    R.p2.set(l, k.n_queue | (k.busy << 16));
+    R.qb.set(l, k.qb);
+    R.cp_lo.set(l, lo32(k.cp_t));
+    R.cp_hi.set(l, hi32(k.cp_t));
+    R.cp_seq.set(l, k.cp_seq);
+    int64_t t = INT64_MAX;
+    uint32_t s = 0xffffffffu, kind = 0;
+    if (k.busy) { t = k.cp_t; s = k.cp_seq; kind = K_COMPLETE; }
     if (k.n_wire) {
-        uint32_t w = (uint32_t)l * S.L->WCAP + ((uint32_t)k.head & (uint32_t)(S.L->WCAP - 1));
-        int64_t t = S.wt[w]; uint32_t s = S.wseq[w];
-        if (key_less(t, s, key.t, key.seq)) { key.t = t; key.seq = s; key.code = (K_ARRIVE << 28) | (uint32_t)l; }
+        uint32_t w = l * (uint32_t)S.L->WCAP + (k.head & (uint32_t)(S.L->WCAP - 1));
+        int64_t wt = u_ld64(S.wt + w);
+        uint32_t ws = u_ld32(S.wseq + w);
+        if (key_less(wt, ws, t, s)) { t = wt; s = ws; kind = K_ARRIVE; }
     }
-    S.lkey[l] = key;
+    R.lk_lo.set(l, lo32(t));
+    R.lk_hi.set(l, hi32(t));
+    R.lk_seq.set(l, s);
+    R.lk_kind.set(l, kind);
 }
 
-__device__ inline void transmit_start(Sim& S, Hot& H, int l, uint32_t ring_idx, uint32_t x) {
+// ---- link FIFO / transmitter (point-to-point-net-device.cc:273-336, 595-666)
+__device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l, LinkV& k, uint32_t ring_idx,
+                                               uint32_t x) {
     const Layout& L = *S.L;
-    LinkState& k = S.ln[l];
-    int64_t tx = l < L.E ? (ent_type(x) == T_DATA ? L.sw_txd : L.sw_txp) : S.acctx[l - L.E];
-    int64_t prop = l < L.E ? L.sw_prop : 0;
+    const bool sw = l < (uint32_t)L.E;
+    int64_t tx = sw ? (ent_type(x) == T_DATA ? L.sw_txd : L.sw_txp) : u_ld64(S.acctx + (l - (uint32_t)L.E));
+    int64_t prop = sw ? L.sw_prop : 0;
     k.busy = 1;
-    k.complete_t = H.now + tx;
-    k.complete_seq = H.seq++;                                  // TransmitComplete
-    uint32_t w = (uint32_t)l * L.WCAP + (ring_idx & (uint32_t)(L.WCAP - 1));
-    S.wt[w] = H.now + tx + prop;
-    S.wseq[w] = H.seq++;                                       // channel Receive
+    k.cp_t = H.now + tx;
+    k.cp_seq = H.seq++;                                        // TransmitComplete
+    uint32_t w = l * (uint32_t)L.WCAP + (ring_idx & (uint32_t)(L.WCAP - 1));
+    int64_t at = H.now + tx + prop;
+    uint32_t as = H.seq++;                                     // channel Receive
+    if (S.lane == 0) { S.wt[w] = at; S.wseq[w] = as; }
     if (k.n_wire > (uint32_t)L.WCAP) fail(H, PRISMA_EBIT_WIRE);
 }
 
-// returns 1 if enqueued, 0 if dropped (or on ring overflow, which fails the replica)
-__device__ inline int link_send(Sim& S, Hot& H, int l, uint4 e) {
+// returns 1 if enqueued, 0 if dropped (a ring overflow fails the replica)
+template <int FS, int LS>
+__device__ __forceinline__ int link_send(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, uint4 e) {
     const Layout& L = *S.L;
-    LinkState& k = S.ln[l];
+    LinkV k = link_get(R, l);
     uint32_t size = ent_size(L, e.x);
-    bool ok = l < L.E ? (k.q_bytes + size <= L.qmax_bytes) : ((uint32_t)k.n_queue + 1u <= L.acc_qmax_pkts);
+    bool ok = l < (uint32_t)L.E ? (k.qb + size <= L.qmax_bytes) : (k.n_queue + 1u <= L.acc_qmax_pkts);
     if (!ok) return 0;
     uint32_t cap = ring_cap(L, l), off = ring_off(L, l);
-    if ((uint32_t)k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
-    uint32_t ti = k.tail;
-    S.ring[off + ti] = e;
-    k.tail = (uint16_t)(ti + 1 == cap ? 0 : ti + 1);
+    if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
+    if (S.lane == 0) S.ring[off + k.tail] = e;
+    k.tail = (k.tail + 1 == cap) ? 0 : k.tail + 1;
     k.n_queue++;
-    k.q_bytes += size;
+    k.qb += size;
     if (!k.busy) {                                              // :643-650
         uint32_t xi = k.txp;
-        uint4 hd = S.ring[off + xi];
-        k.txp = (uint16_t)(xi + 1 == cap ? 0 : xi + 1);
+        uint32_t hx = (k.n_queue == 1) ? e.x : u_ld32(&S.ring[off + xi].x);
+        k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
-        k.q_bytes -= ent_size(L, hd.x);
-        transmit_start(S, H, l, xi, hd.x);
-        relink(S, l);
+        k.qb -= ent_size(L, hx);
+        transmit_start(S, H, l, k, xi, hx);
     }
+    link_put(S, R, l, k);
     return 1;
 }
 
-__device__ inline void on_complete(Sim& S, Hot& H, int l) {         // :305-336
+template <int FS, int LS>
+__device__ __forceinline__ void on_complete(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l) {   // :305-336
     const Layout& L = *S.L;
-    LinkState& k = S.ln[l];
+    LinkV k = link_get(R, l);
     k.busy = 0;
     if (k.n_queue) {
         uint32_t cap = ring_cap(L, l);
         uint32_t xi = k.txp;
-        uint4 hd = S.ring[ring_off(L, l) + xi];
-        k.txp = (uint16_t)(xi + 1 == cap ? 0 : xi + 1);
+        uint32_t hx = u_ld32(&S.ring[ring_off(L, l) + xi].x);
+        k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
-        k.q_bytes -= ent_size(L, hd.x);
-        transmit_start(S, H, l, xi, hd.x);
+        k.qb -= ent_size(L, hx);
+        transmit_start(S, H, l, k, xi, hx);
     }
-    relink(S, l);
+    link_put(S, R, l, k);
 }
 
 // ---- observation (data-packet-manager.cc:171-206)
-__device__ inline uint32_t ping_value(const Sim& S, const Hot& H, int l) {
-    const PingMeta& m = S.pm[l];
+template <int FS, int LS>
+__device__ __forceinline__ uint32_t ping_value(const Sim& S, const Regs<FS, LS>& R, const Hot& H, uint32_t l) {
+    uint32_t pw = R.pm_win.get(l);
+    uint32_t wn = pw & 0xffffu, wh = pw >> 16;
     double avg = 0.0;
-    if (m.win_n > 0) {
+    if (wn > 0) {
         double sum = 0.0;
         uint32_t MA = S.L->ma;
-        uint32_t i = m.win_head;
-        for (uint32_t j = 0; j < m.win_n; ++j) {
-            sum += (double)S.win[(uint32_t)l * MA + i];
+        uint32_t i = wh;
+        for (uint32_t j = 0; j < wn; ++j) {
+            sum += (double)__uint_as_float(u_ld32((const uint32_t*)S.win + l * MA + i));
             i = (i + 1 == MA) ? 0 : i + 1;
         }
-        avg = sum / (double)m.win_n;
+        avg = sum / (double)wn;
     }
     // oldest unacknowledged ping (ping-back-packet-manager.cc:110-116):
     // acknowledgements of one tunnel arrive in index order, so the oldest
     // pending entry is the first hole below the last ack, else the ping
     // after the last ack if it was sent.
+    int32_t hole = (int32_t)R.pm_hole.get(l), acked = (int32_t)R.pm_ack.get(l);
     int64_t oldest = -1;
-    if (m.first_hole >= 0) oldest = m.first_hole;
-    else if ((int64_t)m.acked_last + 1 < (int64_t)H.ping_rounds) oldest = (int64_t)m.acked_last + 1;
+    if (hole >= 0) oldest = hole;
+    else if ((int64_t)acked + 1 < (int64_t)H.ping_rounds) oldest = (int64_t)acked + 1;
     float mt = 0.0f;
     if (oldest >= 0) {
         uint64_t ms = (uint64_t)(((oldest + 1) * S.L->ping_period) / 1000000);
@@ -349,167 +385,190 @@ __device__ inline uint32_t ping_value(const Sim& S, const Hot& H, int l) {
     return (uint32_t)(1000 * mx);
 }
 
-__device__ inline void observe(Sim& S, const Hot& H, int v, uint32_t dst) {
-    const int W = S.L->W;
-    int r0 = S.rowptr[v], r1 = S.rowptr[v + 1];
-    S.obs[0] = dst;
-    for (int i = 1; i < W; ++i) {
-        int l = r0 + i - 1;
-        S.obs[i] = l < r1 ? (S.L->ping_as_obs ? ping_value(S, H, l) : S.ln[l].q_bytes) : 0u;
+// observation words in a per-lane register: lane i holds obs[i]
+template <int FS, int LS>
+__device__ __forceinline__ uint32_t observe(const Sim& S, const Regs<FS, LS>& R, const Hot& H, uint32_t v,
+                                            uint32_t dst) {
+    uint32_t o = (S.lane == 0) ? dst : 0u;
+    int r0 = u_ldi(S.rowptr + v), r1 = u_ldi(S.rowptr + v + 1);
+    for (int l = r0; l < r1; ++l) {
+        uint32_t val = S.L->ping_as_obs ? ping_value(S, R, H, (uint32_t)l) : R.qb.get((uint32_t)l);
+        o = wrl(o, val, (uint32_t)(1 + l - r0));
     }
+    return o;
 }
 
-__device__ inline unsigned char* rec_ptr(const Sim& S, uint32_t d) {
-    return S.logrep + (size_t)(d & (S.L->log_cap - 1)) * S.L->rec_bytes;
-}
-
-__device__ inline void write_record(Sim& S, const Hot& H, uint32_t d, double reward, uint32_t uid, int32_t prev,
-                                    uint32_t node, uint32_t dst, int action, uint32_t status) {
-    unsigned char* p = rec_ptr(S, d);
-    uint4 a, b;
-    a.x = (uint32_t)H.now; a.y = (uint32_t)((uint64_t)H.now >> 32);
+// one coalesced wave store of a decision record (lane i writes word i)
+__device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_t d, double reward, uint32_t uid,
+                                             int32_t prev, uint32_t node, uint32_t dst, int action, uint32_t status,
+                                             uint32_t obs_reg) {
+    const int lane = S.lane;
     uint64_t rb = __double_as_longlong(reward);
-    a.z = (uint32_t)rb; a.w = (uint32_t)(rb >> 32);
-    b.x = uid; b.y = (uint32_t)prev; b.z = node | (dst << 16);
-    b.w = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
-    *(uint4*)(p + 0) = a;
-    *(uint4*)(p + 16) = b;
-    const uint4* o = (const uint4*)S.obs;
-    for (int i = 0; i < S.L->W / 4; ++i) ((uint4*)(p + 32))[i] = o[i];
-    if (S.L->W & 2) *(uint2*)(p + 32 + 16 * (S.L->W / 4)) = *(const uint2*)(S.obs + 4 * (S.L->W / 4));
+    uint32_t w7 = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
+    uint32_t hw;
+    switch (lane) {
+    case 0: hw = lo32(H.now); break;
+    case 1: hw = hi32(H.now); break;
+    case 2: hw = (uint32_t)rb; break;
+    case 3: hw = (uint32_t)(rb >> 32); break;
+    case 4: hw = uid; break;
+    case 5: hw = (uint32_t)prev; break;
+    case 6: hw = node | (dst << 16); break;
+    default: hw = w7; break;
+    }
+    uint32_t ob = (uint32_t)__shfl((int)obs_reg, (lane - 8) & 63);
+    uint32_t word = lane < 8 ? hw : ob;
+    uint32_t* p = (uint32_t*)(S.logrep + (size_t)(d & (S.L->log_cap - 1)) * S.L->rec_bytes);
+    if (lane < 8 + S.L->W) p[lane] = word;
 }
 
-__device__ inline void patch_record(Sim& S, const Hot& H, uint32_t d, int action, uint32_t status) {
-    unsigned char* p = rec_ptr(S, d);
-    *(uint32_t*)(p + 28) = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
+__device__ __forceinline__ void patch_record(const Sim& S, const Hot& H, uint32_t d, int action, uint32_t status) {
+    if (S.lane == 0) {
+        unsigned char* p = S.logrep + (size_t)(d & (S.L->log_cap - 1)) * S.L->rec_bytes;
+        *(uint32_t*)(p + 28) = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
+    }
 }
 
 // Receive tail after the MacRx trace (point-to-point-net-device.cc:430-463)
-__device__ inline void receive_counters(const Layout& L, Hot& H, uint32_t x, int v) {
-    prisma_counters_t& c = H.c;
+__device__ __forceinline__ void receive_counters(const Sim& S, const Hot& H, uint32_t x, uint32_t v) {
+    const Layout& L = *S.L;
     uint32_t type = ent_type(x);
-    if (type == T_DATA && ent_dst(x) == (uint32_t)v) {
-        // valable, nextHop == finalDest on identity overlays
-        c.ov_arrived++;
-        float cost = (float)(ns_to_sec(H.now) - (double)ent_aux(x));
-        c.cost_sum += cost; c.cost_n++;
-        c.e2e_sum += cost; c.e2e_n++;
-    }
-    if (type > 0 && ent_dst(x) == (uint32_t)v) c.bytes_signaling += (int32_t)(L.ping_size - 2);
-    if (type == T_DATA && ent_fresh(x)) {
-        c.ov_injected++;
-        c.bytes_data += (int32_t)(L.data_size - 2);
+    if (S.lane == 0) {
+        prisma_counters_t& c = *S.c;
+        if (type == T_DATA && ent_dst(x) == v) {
+            // valable, nextHop == finalDest on identity overlays
+            c.ov_arrived++;
+            float cost = (float)(ns_to_sec(H.now) - (double)ent_aux(x));
+            c.cost_sum += cost; c.cost_n++;
+            c.e2e_sum += cost; c.e2e_n++;
+        }
+        if (type > 0 && ent_dst(x) == v) c.bytes_signaling += (int32_t)(L.ping_size - 2);
+        if (type == T_DATA && ent_fresh(x)) {
+            c.ov_injected++;
+            c.bytes_data += (int32_t)(L.data_size - 2);
+        }
     }
 }
 
 // DataPacketManager::sendPacket (data-packet-manager.cc:251-299) for the
-// decision held in (e, v, d), then the Receive tail.  `fused` = the record
-// was not written yet (table policy: one record write per decision).
-__device__ inline void apply_decision(Sim& S, Hot& H, uint4 e, int v, uint32_t d, int action, bool fused,
-                                      double reward, int32_t prev) {
+// decision (e, v, d), then the Receive tail.  fused: the record is written
+// here once, with the final status (table policy).
+template <int FS, int LS>
+__device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Hot& H, uint4 e, uint32_t v, uint32_t d,
+                                               int action, bool fused, double reward, int32_t prev,
+                                               uint32_t obs_reg) {
     const Layout& L = *S.L;
-    int r0 = S.rowptr[v], deg = S.rowptr[v + 1] - r0;
+    int r0 = u_ldi(S.rowptr + v), deg = u_ldi(S.rowptr + v + 1) - r0;
     uint32_t status;
     if (action >= 0 && action < deg) {
-        int l = r0 + action;
+        uint32_t l = (uint32_t)(r0 + action);
         uint4 f;
         f.x = ent_make(T_DATA, ent_src(e.x), ent_dst(e.x), 0u, 1u, ent_aux(e.x));
         f.y = e.y;                                   // uid
         f.z = d;                                     // decision of this hop
         f.w = (uint32_t)py_micros(H.now);            // temp_obs time
-        H.c.hops++;
-        H.c.hop_deg_sum += (uint64_t)deg;
-        if (link_send(S, H, l, f)) {
+        CNT(S, hops)++;
+        CNT(S, hop_deg_sum) += (uint64_t)deg;
+        if (link_send(S, R, H, l, f)) {
             status = PRISMA_ST_ENQUEUED;
         } else {
             status = PRISMA_ST_DROPPED;              // :655-664 + forwarder.py:214-244
-            H.c.ov_lost++;
-            H.c.cost_sum += L.loss_penalty_f;
-            H.c.cost_n++;
-            H.c.reward_sum += L.loss_penalty;
+            if (S.lane == 0) {
+                S.c->ov_lost++;
+                S.c->cost_sum += L.loss_penalty_f;
+                S.c->cost_n++;
+                S.c->reward_sum += L.loss_penalty;
+            }
         }
     } else {
         status = PRISMA_ST_DISCARDED;
     }
-    if (fused) write_record(S, H, d, reward, e.y, prev, (uint32_t)v, ent_dst(e.x), action, status);
+    if (fused) write_record(S, H, d, reward, e.y, prev, v, ent_dst(e.x), action, status, obs_reg);
     else patch_record(S, H, d, action, status);
-    receive_counters(L, H, e.x, v);
+    receive_counters(S, H, e.x, v);
 }
 
-__device__ inline void finish_pending(Sim& S, Hot& H, int action) {
-    Hdr& h = *S.h;
-    uint4 e = make_uint4(h.pend_ent[0], h.pend_ent[1], h.pend_ent[2], h.pend_ent[3]);
-    apply_decision(S, H, e, (int)h.pend_node, h.pend_dec, action, false, 0.0, 0);
+template <int FS, int LS>
+__device__ __forceinline__ void finish_pending(const Sim& S, Regs<FS, LS>& R, Hot& H, int action) {
+    const Hdr& h = *S.h;
+    uint4 e = make_uint4(u_ld32(&h.pend_ent[0]), u_ld32(&h.pend_ent[1]), u_ld32(&h.pend_ent[2]),
+                         u_ld32(&h.pend_ent[3]));
+    apply_decision(S, R, H, e, u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action, false, 0.0, 0, 0u);
     H.pend = 0;
 }
 
-// ---- handlers (lane 0) ------------------------------------------------------
-__device__ inline void on_ping_round(Sim& S, Hot& H) {              // data-packet-manager.cc:350-413
+// ---- handlers (uniform) ------------------------------------------------------
+template <int FS, int LS>
+__device__ __forceinline__ void on_ping_round(const Sim& S, Regs<FS, LS>& R, Hot& H) {   // data-packet-manager.cc:350-413
     const Layout& L = *S.L;
     uint32_t k = H.ping_rounds;
     uint32_t ms = (uint32_t)(H.now / 1000000);
     uint32_t first_rearm = 0;
     for (int u = 0; u < L.N; ++u) {
-        int r0 = S.rowptr[u], r1 = S.rowptr[u + 1];
+        int r0 = u_ldi(S.rowptr + u), r1 = u_ldi(S.rowptr + u + 1);
         for (int l = r0; l < r1; ++l) {
             uint4 e;
-            e.x = ent_make(T_PING_FWD, (uint32_t)u, (uint32_t)S.ldst[l], 0u, 0u, (uint32_t)(l - r0));
+            e.x = ent_make(T_PING_FWD, (uint32_t)u, (uint32_t)u_ldi(S.ldst + l), 0u, 0u, (uint32_t)(l - r0));
             e.y = k;
             e.z = ms;
             e.w = 0;
-            if (!link_send(S, H, l, e)) H.c.ctrl_dropped++;
+            if (!link_send(S, R, H, (uint32_t)l, e)) CNT(S, ctrl_dropped)++;
         }
         uint32_t s = H.seq++;                                    // re-arm of node u
         if (u == 0) first_rearm = s;
     }
     H.ping_rounds = k + 1;
     // one ns-3 event per node timer (the round is N consecutive events)
-    H.c.events += (uint64_t)(L.N - 1);
+    CNT(S, events) += (uint64_t)(L.N - 1);
     H.events_total += (uint64_t)(L.N - 1);
     H.ping_t = H.now + L.ping_period;
     H.ping_seq = first_rearm;
 }
 
-__device__ inline void flow_next(Sim& S, Hot& H, int f) {           // poisson-application.cc:265-295
-    uint32_t draw = S.fdraw[f];
-    uint32_t c[4] = { (uint32_t)f, draw, H.episode, 1u };
+template <int FS, int LS>
+__device__ __forceinline__ void flow_next(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t f, uint32_t draw) {
+    uint32_t c[4] = { f, draw, H.episode, 1u };                   // poisson-application.cc:265-295
     philox4x32_10(c, S.L->seed_lo, S.gid);
     uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
     double U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
-    double delay = -S.fmean[f] * det_log(U);
-    S.fdraw[f] = draw + 1;
-    CKey key;
-    key.t = H.now + sec_to_ns(delay);
-    key.seq = H.seq++;
-    key.code = (K_FLOW << 28) | (uint32_t)f;
-    S.fkey[f] = key;
+    double delay = -u_ldd(S.fmean + f) * det_log(U);
+    int64_t t = H.now + sec_to_ns(delay);
+    R.fk_lo.set(f, lo32(t));
+    R.fk_hi.set(f, hi32(t));
+    R.fk_seq.set(f, H.seq++);
+    R.f_draw.set(f, draw + 1);
 }
 
-__device__ inline void on_flow(Sim& S, Hot& H, int f) {
-    if (S.fdraw[f] != 0) {                                          // SendPacket :297-358
-        uint32_t src = (uint32_t)S.fsrc[f];
+template <int FS, int LS>
+__device__ __forceinline__ void on_flow(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t f) {
+    uint32_t draw = R.f_draw.get(f);
+    if (draw != 0) {                                                // SendPacket :297-358
+        uint32_t src = (uint32_t)u_ldi(S.fsrc + f);
         uint4 e;
-        e.x = ent_make(T_DATA, src, (uint32_t)S.fdst[f], 1u, 1u, (uint32_t)(H.now / 1000000000));
+        e.x = ent_make(T_DATA, src, (uint32_t)u_ldi(S.fdst + f), 1u, 1u, (uint32_t)(H.now / 1000000000));
         e.y = H.uid++;
         e.z = 0xffffffffu;
         e.w = 0;
-        link_send(S, H, S.L->E + (int)src, e);                      // access link
+        link_send(S, R, H, (uint32_t)S.L->E + src, e);              // access link
     }
-    flow_next(S, H, f);                                             // StartSending / ScheduleNextTx
+    flow_next(S, R, H, f, draw);                                    // StartSending / ScheduleNextTx
 }
 
-// Returns 1 if a data decision needs an action (its entry/node/record in *pe/*pv/*pd).
-__device__ inline int on_arrive(Sim& S, Hot& H, int l, uint4* pe, int* pv, uint32_t* pd, double* prew,
-                                int32_t* pprev, bool fused) {
+struct Decision {
+    uint4 e; uint32_t v, d; double reward; int32_t prev; uint32_t obs;
+};
+
+// returns 1 if a data decision needs an action
+template <int FS, int LS>
+__device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, Decision& D, bool fused) {
     const Layout& L = *S.L;
-    LinkState& k = S.ln[l];
+    LinkV k = link_get(R, l);
     uint32_t cap = ring_cap(L, l);
-    uint32_t hi = k.head;
-    uint4 e = S.ring[ring_off(L, l) + hi];
-    k.head = (uint16_t)(hi + 1 == cap ? 0 : hi + 1);
+    uint4 e = u_ld128(&S.ring[ring_off(L, l) + k.head]);
+    k.head = (k.head + 1 == cap) ? 0 : k.head + 1;
     k.n_wire--;
-    relink(S, l);
-    int v = S.ldst[l];
+    link_put(S, R, l, k);
+    uint32_t v = (uint32_t)u_ldi(S.ldst + l);
     uint32_t type = ent_type(e.x);
     if (type == T_DATA) {
         // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
@@ -520,178 +579,178 @@ __device__ inline int on_arrive(Sim& S, Hot& H, int l, uint4* pe, int* pv, uint3
         if (!ent_fresh(e.x)) {
             prev = (int32_t)e.z;
             reward = py_reward(H.now, e.w);                        // forwarder.py:360
-            H.c.reward_sum += reward;
+            CNT(S, reward_sum) += reward;
         }
-        observe(S, H, v, dst);
-        H.c.decisions++;
-        if (dst == (uint32_t)v) {                                   // getGameOver
-            write_record(S, H, d, reward, e.y, prev, (uint32_t)v, dst, -1, PRISMA_ST_DESTINATION);
-            receive_counters(L, H, e.x, v);
+        uint32_t o = observe(S, R, H, v, dst);
+        CNT(S, decisions)++;
+        if (dst == v) {                                             // getGameOver
+            write_record(S, H, d, reward, e.y, prev, v, dst, -1, PRISMA_ST_DESTINATION, o);
+            receive_counters(S, H, e.x, v);
             return 0;
         }
-        if (!fused) write_record(S, H, d, reward, e.y, prev, (uint32_t)v, dst, -1, PRISMA_ST_PENDING);
-        *pe = e; *pv = v; *pd = d; *prew = reward; *pprev = prev;
+        if (!fused) write_record(S, H, d, reward, e.y, prev, v, dst, -1, PRISMA_ST_PENDING, o);
+        D.e = e; D.v = v; D.d = d; D.reward = reward; D.prev = prev; D.obs = o;
         return 1;
     }
     if (type == T_PING_FWD) {                                       // ping-forward-packet-manager.cc:94-156
         float delay = (float)(ns_to_sec(H.now) - ((double)e.z * 0.001));
         uint4 b;
-        b.x = ent_make(T_PING_BACK, (uint32_t)v, ent_src(e.x), 0u, 0u, ent_aux(e.x));
+        b.x = ent_make(T_PING_BACK, v, ent_src(e.x), 0u, 0u, ent_aux(e.x));
         b.y = e.y;
-        b.z = __float_as_uint(delay);
+        b.z = rfl(__float_as_uint(delay));
         b.w = 0;
-        if (!link_send(S, H, S.lrev[l], b)) H.c.ctrl_dropped++;
+        if (!link_send(S, R, H, (uint32_t)u_ldi(S.lrev + l), b)) CNT(S, ctrl_dropped)++;
     } else if (type == T_PING_BACK) {                               // ping-back-packet-manager.cc:120-144
-        int lt = S.rowptr[v] + (int)ent_aux(e.x);
-        PingMeta& m = S.pm[lt];
+        uint32_t lt = (uint32_t)(u_ldi(S.rowptr + v) + (int32_t)ent_aux(e.x));
+        int32_t acked = (int32_t)R.pm_ack.get(lt), hole = (int32_t)R.pm_hole.get(lt);
         int32_t idx = (int32_t)e.y;
-        if (idx <= m.acked_last) {
+        if (idx <= acked) {
             fail(H, PRISMA_EBIT_ACKORDER);
         } else {
-            if (idx > m.acked_last + 1 && m.first_hole < 0) m.first_hole = m.acked_last + 1;
-            m.acked_last = idx;
+            if (idx > acked + 1 && hole < 0) R.pm_hole.set(lt, (uint32_t)(acked + 1));
+            R.pm_ack.set(lt, (uint32_t)idx);
         }
         uint32_t MA = L.ma;
-        uint32_t slot;
-        if (m.win_n >= MA) {
-            slot = m.win_head;
-            m.win_head = (m.win_head + 1 == MA) ? 0 : m.win_head + 1;
+        uint32_t pw = R.pm_win.get(lt);
+        uint32_t wn = pw & 0xffffu, wh = pw >> 16, slot;
+        if (wn >= MA) {
+            slot = wh;
+            wh = (wh + 1 == MA) ? 0 : wh + 1;
         } else {
-            slot = m.win_head + m.win_n;
+            slot = wh + wn;
             if (slot >= MA) slot -= MA;
-            m.win_n++;
+            wn++;
         }
-        S.win[(uint32_t)lt * MA + slot] = __uint_as_float(e.z);
+        R.pm_win.set(lt, wn | (wh << 16));
+        if (S.lane == 0) S.win[lt * MA + slot] = __uint_as_float(e.z);
     }
-    receive_counters(L, H, e.x, v);
+    receive_counters(S, H, e.x, v);
     return 0;
 }
 
 // ---------------------------------------------------------------------------
-// replica (re)initialisation: all lanes, operates on the LDS image
+// replica (re)initialisation: LDS image zeroed, registers set (all lanes)
 // ---------------------------------------------------------------------------
-__device__ void init_replica(Sim& S, int lane, uint32_t episode) {
+template <int FS, int LS>
+__device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t episode) {
     const Layout& L = *S.L;
-    uint32_t dec = S.h->dec_count;                 // monotonic across episodes
-    uint64_t ht = S.h->hops_total, et = S.h->events_total;
-    uint32_t hl = S.h->hops_launch;                // per-launch budget survives resets
+    const int lane = S.lane;
+    uint32_t dec = H.dec, hl = H.hops_launch;
+    uint64_t ht = H.hops_total, et = H.events_total;
     __syncthreads();
     uint4* st4 = (uint4*)(S.base + L.topo_bytes);
-    for (uint32_t i = (uint32_t)lane; i < L.state_bytes / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
-    __syncthreads();
-    for (int f = lane; f < L.F; f += kWave) {
-        uint32_t c[4] = { (uint32_t)f, 0u, episode, 0u };
-        philox4x32_10(c, L.seed_lo, S.gid);
-        uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
-        double U = (double)u53 * (1.0 / 9007199254740992.0);
-        CKey key;
-        key.t = sec_to_ns(0.0001 + U);                             // sim.cc:610-630
-        key.seq = (uint32_t)(L.N + f);
-        key.code = (K_FLOW << 28) | (uint32_t)f;
-        S.fkey[f] = key;
-        S.fdraw[f] = 0;
+    for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < FS; ++j) {
+        uint32_t f = (uint32_t)lane + 64u * j;
+        int64_t t = INT64_MAX;
+        uint32_t s = 0xffffffffu;
+        if (f < (uint32_t)L.F) {
+            uint32_t c[4] = { f, 0u, episode, 0u };
+            philox4x32_10(c, L.seed_lo, S.gid);
+            uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
+            double U = (double)u53 * (1.0 / 9007199254740992.0);
+            t = sec_to_ns(0.0001 + U);                              // sim.cc:610-630
+            s = (uint32_t)L.N + f;
+        }
+        R.fk_lo.v[j] = lo32(t); R.fk_hi.v[j] = hi32(t); R.fk_seq.v[j] = s; R.f_draw.v[j] = 0;
     }
-    for (int l = lane; l < L.E; l += kWave) {
-        S.pm[l].acked_last = -1;
-        S.pm[l].first_hole = -1;
+#pragma unroll
+    for (int j = 0; j < LS; ++j) {
+        R.lk_lo.v[j] = lo32(INT64_MAX); R.lk_hi.v[j] = hi32(INT64_MAX); R.lk_seq.v[j] = 0xffffffffu;
+        R.lk_kind.v[j] = 0; R.cp_lo.v[j] = 0; R.cp_hi.v[j] = 0; R.cp_seq.v[j] = 0;
+        R.p0.v[j] = 0; R.p1.v[j] = 0; R.p2.v[j] = 0; R.qb.v[j] = 0;
+        R.pm_ack.v[j] = 0xffffffffu; R.pm_hole.v[j] = 0xffffffffu; R.pm_win.v[j] = 0;
     }
-    for (int l = lane; l < L.L; l += kWave) {
-        CKey key;
-        key.t = INT64_MAX; key.seq = 0xffffffffu; key.code = 0xffffffffu;
-        S.lkey[l] = key;
-    }
-    if (lane == 0) {
-        Hdr& h = *S.h;
-        h.now = 0;
-        h.ping_t = L.ping_period;                                  // data-packet-manager.cc:118-121
-        h.ping_seq = 0;
-        h.seq = (uint32_t)(L.N + L.F);
-        h.dec_count = dec;
-        h.hops_total = ht;
-        h.events_total = et;
-        h.hops_launch = hl;
-        h.episode = episode;
-        S.c->episode = episode;
-    }
+    H.now = 0;
+    H.ping_t = L.ping_period;                                       // data-packet-manager.cc:118-121
+    H.ping_seq = 0;
+    H.seq = (uint32_t)L.N + (uint32_t)L.F;
+    H.uid = 0; H.ping_rounds = 0; H.pend = 0; H.over = 0; H.error = 0; H.stop = 0;
+    H.dec = dec; H.hops_launch = hl; H.hops_total = ht; H.events_total = et;
+    H.episode = episode;
+    if (lane == 0) S.c->episode = episode;
     __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
-// wave-wide event selection: per-lane min over owned candidate keys, then a
-// DPP reduction of the 64-bit time to lane 63; the (rare) same-ns ties are
-// resolved by a second reduction of seq over the tied lanes.
+// wave-wide event selection: per-lane min over owned register keys, a DPP
+// reduction of the 64-bit time to lane 63, and a second reduction of seq over
+// the tied lanes only when two sources share the nanosecond.
 // ---------------------------------------------------------------------------
 template <int CTRL, int ROW_MASK>
-__device__ inline uint32_t dpp_u32(uint32_t v) {
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xf, false);
 }
 
 template <int CTRL, int ROW_MASK>
-__device__ inline int64_t dpp_min_i64(int64_t v) {
-    uint32_t lo = dpp_u32<CTRL, ROW_MASK>((uint32_t)v);
-    uint32_t hi = dpp_u32<CTRL, ROW_MASK>((uint32_t)((uint64_t)v >> 32));
-    int64_t o = (int64_t)(((uint64_t)hi << 32) | lo);
+__device__ __forceinline__ int64_t dpp_min_i64(int64_t v) {
+    uint32_t lo = dpp_u32<CTRL, ROW_MASK>(lo32(v));
+    uint32_t hi = dpp_u32<CTRL, ROW_MASK>(hi32(v));
+    int64_t o = mk64(lo, hi);
     return o < v ? o : v;
 }
 
 template <int CTRL, int ROW_MASK>
-__device__ inline uint32_t dpp_min_u32(uint32_t v) {
+__device__ __forceinline__ uint32_t dpp_min_u32(uint32_t v) {
     uint32_t o = dpp_u32<CTRL, ROW_MASK>(v);
     return o < v ? o : v;
 }
 
-__device__ inline int64_t wave_min_i64(int64_t v) {
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
     v = dpp_min_i64<0xB1, 0xF>(v);      // quad_perm [1,0,3,2]
     v = dpp_min_i64<0x4E, 0xF>(v);      // quad_perm [2,3,0,1]
     v = dpp_min_i64<0x141, 0xF>(v);     // row_half_mirror
     v = dpp_min_i64<0x140, 0xF>(v);     // row_mirror
     v = dpp_min_i64<0x142, 0xA>(v);     // row_bcast:15
     v = dpp_min_i64<0x143, 0xC>(v);     // row_bcast:31
-    uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
-    uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), 63);
-    return (int64_t)(((uint64_t)hi << 32) | lo);
+    return mk64(rdl(lo32(v), 63), rdl(hi32(v), 63));
 }
 
-__device__ inline uint32_t wave_min_u32(uint32_t v) {
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     v = dpp_min_u32<0xB1, 0xF>(v);
     v = dpp_min_u32<0x4E, 0xF>(v);
     v = dpp_min_u32<0x141, 0xF>(v);
     v = dpp_min_u32<0x140, 0xF>(v);
     v = dpp_min_u32<0x142, 0xA>(v);
     v = dpp_min_u32<0x143, 0xC>(v);
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+    return rdl(v, 63);
 }
 
-__device__ inline void select_event(const Sim& S, const Hot& H, int lane, int64_t& bt, uint32_t& bc) {
-    const Layout& L = *S.L;
+template <int FS, int LS>
+__device__ __forceinline__ void select_event(const Regs<FS, LS>& R, const Hot& H, int lane, int64_t& bt, uint32_t& bc) {
     int64_t t = INT64_MAX;
     uint32_t s = 0xffffffffu, c = 0xffffffffu;
-    for (int f = lane; f < L.F; f += kWave) {
-        CKey k = S.fkey[f];
-        if (key_less(k.t, k.seq, t, s)) { t = k.t; s = k.seq; c = k.code; }
+#pragma unroll
+    for (int j = 0; j < FS; ++j) {
+        int64_t tj = mk64(R.fk_lo.v[j], R.fk_hi.v[j]);
+        uint32_t sj = R.fk_seq.v[j];
+        if (key_less(tj, sj, t, s)) { t = tj; s = sj; c = (K_FLOW << 28) | (uint32_t)(lane + 64 * j); }
     }
-    for (int l = lane; l < L.L; l += kWave) {
-        CKey k = S.lkey[l];
-        if (key_less(k.t, k.seq, t, s)) { t = k.t; s = k.seq; c = k.code; }
+#pragma unroll
+    for (int j = 0; j < LS; ++j) {
+        int64_t tj = mk64(R.lk_lo.v[j], R.lk_hi.v[j]);
+        uint32_t sj = R.lk_seq.v[j];
+        if (key_less(tj, sj, t, s)) { t = tj; s = sj; c = (R.lk_kind.v[j] << 28) | (uint32_t)(lane + 64 * j); }
     }
     if (lane == 0 && key_less(H.ping_t, H.ping_seq, t, s)) { t = H.ping_t; s = H.ping_seq; c = K_PING << 28; }
     const int64_t tmin = wave_min_i64(t);
     uint64_t tied = __ballot(t == tmin);
-    int win;
+    uint32_t win;
     if ((tied & (tied - 1)) == 0) {
-        win = __builtin_ctzll(tied);
+        win = (uint32_t)__builtin_ctzll(tied);
     } else {                                                        // same-ns events: ns-3 uid order
         uint32_t smin = wave_min_u32(t == tmin ? s : 0xffffffffu);
-        win = __builtin_ctzll(__ballot(t == tmin && s == smin));
+        win = (uint32_t)__builtin_ctzll(__ballot(t == tmin && s == smin));
     }
     bt = tmin;
-    bc = (uint32_t)__builtin_amdgcn_readlane((int)c, win);
+    bc = rdl(c, win);
 }
 
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
-__device__ inline void stage_in(unsigned char* lds, const KParams& P, int r, int lane) {
+__device__ __forceinline__ void stage_topo(unsigned char* lds, const KParams& P, int lane) {
     const Layout& L = P.lay;
     const uint4* t4 = (const uint4*)P.topo;
     uint4* l4 = (uint4*)lds;
@@ -701,135 +760,157 @@ __device__ inline void stage_in(unsigned char* lds, const KParams& P, int r, int
         const uint32_t nt = (uint32_t)(L.N * L.N);
         for (uint32_t i = (uint32_t)lane; i < nt; i += kWave) dstp[i] = P.table[i];
     }
-    const uint4* s4 = (const uint4*)(P.state + (size_t)r * L.state_bytes);
-    uint4* d4 = (uint4*)(lds + L.topo_bytes);
-    for (uint32_t i = (uint32_t)lane; i < L.state_bytes / 16u; i += kWave) d4[i] = s4[i];
 }
 
-__device__ inline void stage_out(unsigned char* lds, const KParams& P, int r, int lane) {
+template <int FS, int LS>
+__device__ __forceinline__ void stage_in(unsigned char* lds, const KParams& P, int r, int lane, Regs<FS, LS>& R) {
     const Layout& L = P.lay;
-    uint4* s4 = (uint4*)(P.state + (size_t)r * L.state_bytes);
-    const uint4* d4 = (const uint4*)(lds + L.topo_bytes);
-    for (uint32_t i = (uint32_t)lane; i < L.state_bytes / 16u; i += kWave) s4[i] = d4[i];
+    stage_topo(lds, P, lane);
+    const unsigned char* img = P.state + (size_t)r * L.state_bytes;
+    const uint4* s4 = (const uint4*)img;
+    uint4* d4 = (uint4*)(lds + L.topo_bytes);
+    for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes / 16u; i += kWave) d4[i] = s4[i];
+    regs_io(R, (uint32_t*)(const_cast<unsigned char*>(img) + L.s_regs), lane, false);
 }
 
-__device__ inline void publish_counters(Sim& S, const KParams& P, int r, int lane) {
+template <int FS, int LS>
+__device__ __forceinline__ void stage_out(unsigned char* lds, const KParams& P, int r, int lane, Regs<FS, LS>& R) {
+    const Layout& L = P.lay;
+    unsigned char* img = P.state + (size_t)r * L.state_bytes;
+    uint4* s4 = (uint4*)img;
+    const uint4* d4 = (const uint4*)(lds + L.topo_bytes);
+    for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes / 16u; i += kWave) s4[i] = d4[i];
+    regs_io(R, (uint32_t*)(img + L.s_regs), lane, true);
+}
+
+__device__ __forceinline__ void publish_counters(const Sim& S, const KParams& P, int r, int lane) {
     const uint32_t* src = (const uint32_t*)S.c;
     uint32_t* dst = (uint32_t*)(P.cnt_out + r);
     if (lane < (int)(sizeof(prisma_counters_t) / 4)) dst[lane] = src[lane];
 }
 
-extern "C" __global__ void __launch_bounds__(64) prisma_reset_kernel(KParams P) {
+template <int FS, int LS>
+__global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
     const Layout& L = P.lay;
-    const uint4* t4 = (const uint4*)P.topo;
-    uint4* l4 = (uint4*)lds;
-    for (uint32_t i = (uint32_t)lane; i < L.topo_bytes / 16u; i += kWave) l4[i] = t4[i];
+    stage_topo(lds, P, lane);
+    __syncthreads();
     Sim S;
-    sim_bind(S, L, lds, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r);
-    if (lane == 0) { S.h->dec_count = 0; S.h->hops_total = 0; S.h->events_total = 0; S.h->hops_launch = 0; }
-    init_replica(S, lane, P.episode);
-    if (lane == 0) {
-        Hot H;
-        hot_load(S, H);
-        hot_store(S, H);
-    }
+    sim_bind(S, L, lds, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r, lane);
+    Regs<FS, LS> R;
+    Hot H;
+    memset(&H, 0, sizeof(H));
+    init_replica(S, R, H, P.episode);
+    hot_store(S, H);
     __syncthreads();
     publish_counters(S, P, r, lane);
-    stage_out(lds, P, r, lane);
+    stage_out(lds, P, r, lane, R);
 }
 
-extern "C" __global__ void __launch_bounds__(64) prisma_step_kernel(KParams P) {
+template <int FS, int LS>
+__global__ void __launch_bounds__(64) prisma_step_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
     const Layout& L = P.lay;
-    stage_in(lds, P, r, lane);
+    Regs<FS, LS> R;
+    stage_in(lds, P, r, lane, R);
     __syncthreads();
     Sim S;
-    sim_bind(S, L, lds, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r);
+    sim_bind(S, L, lds, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r, lane);
     const bool table_mode = (P.mode == 2);
     const uint32_t max_hops = (uint32_t)P.max_hops;
     const uint32_t NN = (uint32_t)L.N;
     Hot H;
-    hot_load(S, H);                                    // every lane holds a copy; lane 0 owns it
+    hot_load(S, H);
 
-    if (lane == 0) {
-        H.stop = 0;
-        H.hops_launch = 0;
-        if (H.pend && !H.over) {
-            if (table_mode) {
-                finish_pending(S, H, (int)S.table[S.h->pend_node * NN + ent_dst(S.h->pend_ent[0])]);
-                H.hops_launch++;
-                H.hops_total++;
-            } else if (P.actions) {
-                finish_pending(S, H, (int)P.actions[r]);
-            } else {
-                H.stop = 1;                            // nothing to apply: re-emit the pending obs
-            }
+    H.stop = 0;
+    H.hops_launch = 0;
+    if (H.pend && !H.over) {
+        if (table_mode) {
+            uint32_t pn = u_ld32(&S.h->pend_node), pd = ent_dst(u_ld32(&S.h->pend_ent[0]));
+            finish_pending(S, R, H, (int)rfl((uint32_t)S.table[pn * NN + pd]));
+            H.hops_launch++;
+            H.hops_total++;
+        } else if (P.actions) {
+            finish_pending(S, R, H, (int)rfl((uint32_t)P.actions[r]));
+        } else {
+            H.stop = 1;                                // nothing to apply: re-emit the pending obs
         }
-        if (H.over || (table_mode && H.hops_launch >= max_hops)) H.stop = 1;
     }
-    __syncthreads();
-    uint32_t stop = (uint32_t)__builtin_amdgcn_readfirstlane((int)H.stop);
+    if (H.over || (table_mode && H.hops_launch >= max_hops)) H.stop = 1;
+
     uint32_t resets = 0;
-    while (!stop) {
+    while (!H.stop) {
         int64_t bt;
         uint32_t bc;
-        select_event(S, H, lane, bt, bc);
+        select_event(R, H, lane, bt, bc);
         if (bt >= L.t_end) {                           // Simulator::Stop(simTime) (sim.cc:703)
             if (L.auto_reset && resets < 64u) {        // bounded: an empty scenario cannot spin forever
                 ++resets;
-                if (lane == 0) hot_store(S, H);
-                init_replica(S, lane, H.episode + 1u);
-                hot_load(S, H);
+                init_replica(S, R, H, H.episode + 1u);
                 continue;
             }
-            if (lane == 0) { H.over = 1; H.stop = 1; }
+            H.over = 1;
+            H.stop = 1;
             break;
         }
-        if (lane == 0) {
-            H.now = bt;
-            H.c.events++;
-            H.events_total++;
-            const uint32_t kind = bc >> 28, id = bc & 0x0fffffffu;
-            if (kind == K_ARRIVE) {
-                uint4 e; int v; uint32_t d; double rw; int32_t pv;
-                if (on_arrive(S, H, (int)id, &e, &v, &d, &rw, &pv, table_mode)) {
-                    if (table_mode) {
-                        apply_decision(S, H, e, v, d, (int)S.table[(uint32_t)v * NN + ent_dst(e.x)], true, rw, pv);
-                        H.hops_launch++;
-                        H.hops_total++;
-                        if (H.hops_launch >= max_hops) H.stop = 1;
-                    } else {
+        H.now = bt;
+        CNT(S, events)++;
+        H.events_total++;
+        const uint32_t kind = bc >> 28, id = bc & 0x0fffffffu;
+        if (kind == K_ARRIVE) {
+            Decision D;
+            if (on_arrive(S, R, H, id, D, table_mode)) {
+                if (table_mode) {
+                    int a = (int)S.table[D.v * NN + ent_dst(D.e.x)];
+                    apply_decision(S, R, H, D.e, D.v, D.d, (int)rfl((uint32_t)a), true, D.reward, D.prev, D.obs);
+                    H.hops_launch++;
+                    H.hops_total++;
+                    if (H.hops_launch >= max_hops) H.stop = 1;
+                } else {
+                    if (lane == 0) {
                         Hdr& h = *S.h;
-                        h.pend_link = id; h.pend_node = (uint32_t)v; h.pend_dec = d;
-                        h.pend_ent[0] = e.x; h.pend_ent[1] = e.y; h.pend_ent[2] = e.z; h.pend_ent[3] = e.w;
-                        H.pend = 1;
-                        H.stop = 1;
+                        h.pend_link = id; h.pend_node = D.v; h.pend_dec = D.d;
+                        h.pend_ent[0] = D.e.x; h.pend_ent[1] = D.e.y; h.pend_ent[2] = D.e.z; h.pend_ent[3] = D.e.w;
                     }
+                    if (lane < L.W) S.obs[lane] = D.obs;
+                    H.pend = 1;
+                    H.stop = 1;
                 }
-            } else if (kind == K_COMPLETE) {
-                on_complete(S, H, (int)id);
-            } else if (kind == K_FLOW) {
-                on_flow(S, H, (int)id);
-            } else {
-                on_ping_round(S, H);
             }
-            if (H.error) { H.over = 1; H.stop = 1; }
+        } else if (kind == K_COMPLETE) {
+            on_complete(S, R, H, id);
+        } else if (kind == K_FLOW) {
+            on_flow(S, R, H, id);
+        } else {
+            on_ping_round(S, R, H);
         }
-        __syncthreads();
-        stop = (uint32_t)__builtin_amdgcn_readfirstlane((int)H.stop);
+        if (H.error) { H.over = 1; H.stop = 1; }
     }
 
-    if (lane == 0) hot_store(S, H);
+    hot_store(S, H);
     __syncthreads();
-    const bool pending = S.h->pend && !S.h->over;
+    const bool pending = H.pend && !H.over;
     if (P.mask_out && lane == 0) P.mask_out[r] = pending ? 1 : 0;
     if (P.node_out && lane == 0) P.node_out[r] = pending ? (int32_t)S.h->pend_node : -1;
     if (P.obs_out && lane < L.W) P.obs_out[(size_t)r * L.W + lane] = pending ? (int32_t)S.obs[lane] : 0;
     publish_counters(S, P, r, lane);
-    stage_out(lds, P, r, lane);
+    stage_out(lds, P, r, lane, R);
+}
+
+// instantiations: flow slots FS in {1,2,4,8} (F <= 512), link slots LS in {1,2,4} (L <= 256)
+typedef void (*kernel_fn)(KParams);
+template <int FS, int LS> struct KPair {
+    static const void* step() { return (const void*)prisma_step_kernel_t<FS, LS>; }
+    static const void* reset() { return (const void*)prisma_reset_kernel_t<FS, LS>; }
+};
+
+static const void* pick_kernel(int fs, int ls, bool reset) {
+#define PK(F_, L_) if (fs == F_ && ls == L_) return reset ? KPair<F_, L_>::reset() : KPair<F_, L_>::step();
+    PK(1, 1) PK(1, 2) PK(1, 4) PK(2, 1) PK(2, 2) PK(2, 4) PK(4, 1) PK(4, 2) PK(4, 4) PK(8, 1) PK(8, 2) PK(8, 4)
+#undef PK
+    return nullptr;
 }
 
 // Gather records (replica[i], dec[i]) into a dense array: one lane per 4-byte
@@ -861,6 +942,8 @@ struct prisma_env {
     unsigned char* d_topo = nullptr;
     unsigned char* d_log = nullptr;
     prisma_counters_t* d_cnt = nullptr;
+    const void* k_step = nullptr;
+    const void* k_reset = nullptr;
     bool reset_done = false;
 };
 
@@ -974,22 +1057,25 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
         fmean[f] = (double)(P->packet_size * 8u) / (double)T->flow_rate_bps[f];
     memcpy(&topo[L.t_fmean], fmean.data(), 8u * F);
 
-    // state image
+    // state image: LDS part (staged into LDS) then register part (staged into VGPRs)
+    int fs = 1, ls = 1;
+    while (64 * fs < F) fs *= 2;
+    while (64 * ls < Lk) ls *= 2;
+    if (fs > 8 || ls > 4)
+        return set_err(PRISMA_ERR_CONFIG, "more than 512 flows or 256 links per replica (register-resident engine)");
+    L.FS = fs; L.LS = ls;
     o = 0;
     L.s_hdr = take(sizeof(Hdr));
     L.s_cnt = take(sizeof(prisma_counters_t));
     L.s_obs = take(4u * L.W);
-    L.s_fkey = take(16u * F);
-    L.s_fdraw = take(4u * F);
-    L.s_lkey = take(16u * Lk);
-    L.s_link = take(sizeof(LinkState) * Lk);
     L.s_wt = take(8u * Lk * L.WCAP);
     L.s_wseq = take(4u * Lk * L.WCAP);
     L.s_ring = take(16u * tot);
     L.s_win = take(4u * E * L.MA);
-    L.s_pmeta = take(sizeof(PingMeta) * E);
+    L.lds_state_bytes = o;
+    L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 14u * 64u * (uint32_t)ls));
     L.state_bytes = o;
-    L.lds_bytes = L.topo_bytes + L.state_bytes;
+    L.lds_bytes = L.topo_bytes + L.lds_state_bytes;
     if (L.lds_bytes > 160u * 1024u)
         return set_err(PRISMA_ERR_CONFIG, "replica state exceeds the 160 KiB LDS of a gfx950 CU");
 
@@ -1042,8 +1128,10 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
         prisma_destroy(e);
         return set_err(PRISMA_ERR_DEVICE, "device initialisation failed");
     }
-    (void)hipFuncSetAttribute((const void*)prisma_step_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
-    (void)hipFuncSetAttribute((const void*)prisma_reset_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
+    e->k_step = pick_kernel(L.FS, L.LS, false);
+    e->k_reset = pick_kernel(L.FS, L.LS, true);
+    (void)hipFuncSetAttribute(e->k_step, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
+    (void)hipFuncSetAttribute(e->k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
     *out = e;
     return PRISMA_OK;
 }
@@ -1074,7 +1162,7 @@ extern "C" int prisma_reset(prisma_env_t* e, uint32_t episode, void* stream) {
     KParams P = base_params(e);
     P.mode = 0;
     P.episode = episode;
-    int rc = launch(e, (const void*)prisma_reset_kernel, P, stream);
+    int rc = launch(e, e->k_reset, P, stream);
     if (!rc) e->reset_done = true;
     return rc;
 }
@@ -1090,7 +1178,7 @@ extern "C" int prisma_step(prisma_env_t* e, const int32_t* actions, int32_t* obs
     P.mask_out = mask_out;
     P.node_out = node_out;
     P.max_hops = 0x7fffffff;
-    return launch(e, (const void*)prisma_step_kernel, P, stream);
+    return launch(e, e->k_step, P, stream);
 }
 
 extern "C" int prisma_run(prisma_env_t* e, int32_t policy, const uint8_t* table, int32_t max_hops, void* stream) {
@@ -1102,7 +1190,7 @@ extern "C" int prisma_run(prisma_env_t* e, int32_t policy, const uint8_t* table,
     P.mode = 2;
     P.table = table;
     P.max_hops = max_hops;
-    return launch(e, (const void*)prisma_step_kernel, P, stream);
+    return launch(e, e->k_step, P, stream);
 }
 
 extern "C" int prisma_read_counters(prisma_env_t* e, prisma_counters_t* host_out, void* stream) {
