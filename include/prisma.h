@@ -73,6 +73,7 @@ extern "C" {
 #define PRISMA_EBIT_WIRE       2u  /* more packets on a wire than sized    */
 #define PRISMA_EBIT_ACKORDER   4u  /* ping-back arrived out of order       */
 #define PRISMA_EBIT_TIME       8u  /* time beyond the representable range  */
+#define PRISMA_EBIT_LOGWRAP   16u  /* a hop outlived log_capacity decisions */
 
 /*
  * Topology of one replica (identity overlay: every underlay node is an
@@ -112,7 +113,9 @@ typedef struct prisma_params {
     double   loss_penalty;      /* ((16260+542)*8/cap+0.001)*N             */
     uint64_t seed;              /* simSeed                     [100]       */
     uint32_t replica_base;      /* global id of replica 0 (multi-GPU)      */
-    uint32_t log_capacity;      /* records kept per replica (power of 2)   */
+    uint32_t log_capacity;      /* records kept per replica (power of 2,
+                                   >= 1024; must exceed the decisions made
+                                   while one packet crosses one link)      */
 } prisma_params_t;
 
 /*
@@ -130,9 +133,9 @@ typedef struct prisma_params {
  */
 typedef struct prisma_record {
     int64_t  t_ns;
-    double   reward;
     uint32_t uid;
     int32_t  prev;
+    double   reward;
     uint16_t node;
     uint16_t dst;
     int8_t   action;

@@ -109,7 +109,7 @@ static double py_reward(int64_t t1, int64_t t0) {
 /* record / counter layouts (byte-identical to include/prisma.h)       */
 /* ------------------------------------------------------------------ */
 typedef struct {
-    int64_t t_ns; double reward; uint32_t uid; int32_t prev;
+    int64_t t_ns; uint32_t uid; int32_t prev; double reward;
     uint16_t node; uint16_t dst; int8_t action; uint8_t status; uint16_t episode;
 } rec_head_t;
 

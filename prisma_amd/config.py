@@ -73,8 +73,8 @@ def engine_params(topo: Topology, *, sim_time_s: float = 60.0, seed: int = 100, 
     if train:
         raise NotImplementedError("train=1 small-signalling echoes (SURVEY 8a A14) are not modelled; "
                                   "parity configs use train=0")
-    if log_capacity & (log_capacity - 1):
-        raise ValueError("log_capacity must be a power of two")
+    if log_capacity < 1024 or log_capacity & (log_capacity - 1):
+        raise ValueError("log_capacity must be a power of two >= 1024")
     lp = _loss_penalty(max_buffer, packet_size, link_cap, topo.n_nodes) if loss_penalty is None else loss_penalty
     return dict(
         link_bps=int(link_cap), link_delay_ns=int(round(link_delay_ms * 1e6)),

@@ -14,19 +14,24 @@ constexpr uint32_t K_PING = 0u, K_FLOW = 1u, K_COMPLETE = 2u, K_ARRIVE = 3u;
 // packet types (enum-and-constants.h:5-11)
 constexpr uint32_t T_DATA = 0u, T_PING_FWD = 3u, T_PING_BACK = 4u;
 
-// packet entry (16 bytes) fields, word x:
-//   bits 0-2 type | 3-10 src | 11-18 dst | 19 fresh (lastHop==1000) |
-//   20 valable | 21-31: data -> start second (11 bits), ping -> tunnel (8 bits)
-// y: data uid, ping index;  z: data prev decision, ping-fwd start_ms,
-// ping-back one-hop delay (f32 bits);  w: data decision time in us.
+// 8-byte packet entry (uint2) of a link ring:
+//   data: x = type(3) | dst(8) << 3 | fresh(1) << 11 | start second(12) << 12
+//         y = decision index of the previous hop (fresh packet: its uid)
+//   ping: x = type(3) | tunnel(8) << 3 | round(21) << 11
+//         y = ping-back one-hop delay (f32 bits)
+// The uid and decision time of a forwarded packet are read back from its
+// previous decision record in the HBM log when it arrives.
 __host__ __device__ inline uint32_t ent_type(uint32_t x) { return x & 7u; }
-__host__ __device__ inline uint32_t ent_src(uint32_t x) { return (x >> 3) & 255u; }
-__host__ __device__ inline uint32_t ent_dst(uint32_t x) { return (x >> 11) & 255u; }
-__host__ __device__ inline uint32_t ent_fresh(uint32_t x) { return (x >> 19) & 1u; }
-__host__ __device__ inline uint32_t ent_aux(uint32_t x) { return x >> 21; }
-__host__ __device__ inline uint32_t ent_make(uint32_t type, uint32_t src, uint32_t dst, uint32_t fresh,
-                                             uint32_t valable, uint32_t aux) {
-    return type | (src << 3) | (dst << 11) | (fresh << 19) | (valable << 20) | (aux << 21);
+__host__ __device__ inline uint32_t d_dst(uint32_t x) { return (x >> 3) & 255u; }
+__host__ __device__ inline uint32_t d_fresh(uint32_t x) { return (x >> 11) & 1u; }
+__host__ __device__ inline uint32_t d_start(uint32_t x) { return x >> 12; }
+__host__ __device__ inline uint32_t p_tunnel(uint32_t x) { return (x >> 3) & 255u; }
+__host__ __device__ inline uint32_t p_round(uint32_t x) { return x >> 11; }
+__host__ __device__ inline uint32_t d_make(uint32_t dst, uint32_t fresh, uint32_t start_s) {
+    return T_DATA | (dst << 3) | (fresh << 11) | (start_s << 12);
+}
+__host__ __device__ inline uint32_t p_make(uint32_t type, uint32_t tunnel, uint32_t round) {
+    return type | (tunnel << 3) | (round << 11);
 }
 
 struct Hdr {                 // 128 bytes at state offset 0

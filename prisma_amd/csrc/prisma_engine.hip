@@ -111,7 +111,9 @@ struct Regs {
     LA<LS> cp_lo, cp_hi, cp_seq;                 // tx completion event (valid while busy)
     LA<LS> p0, p1, p2, qb;                       // head|txp<<16, tail|n_wire<<16, n_queue|busy<<16, queued bytes
     LA<LS> pm_ack, pm_hole, pm_win;              // ping: last ack, first hole, win_n|win_head<<16
-    static constexpr int NF = 4, NL = 14;
+    LA<LS> pav_lo, pav_hi;                       // ping window mean (double), refreshed per ping-back
+    LA<LS> nd_lo, nd_hi, hd_lo, hd_hi;           // send time (s) of ping ack+1 and of the first hole
+    static constexpr int NF = 4, NL = 20;
 };
 
 template <int FS, int LS>
@@ -123,7 +125,8 @@ __device__ __forceinline__ void regs_io(Regs<FS, LS>& R, uint32_t* img, int lane
     RIO_F(fk_lo, 0) RIO_F(fk_hi, 1) RIO_F(fk_seq, 2) RIO_F(f_draw, 3)
     RIO_L(lk_lo, 0) RIO_L(lk_hi, 1) RIO_L(lk_seq, 2) RIO_L(lk_kind, 3) RIO_L(cp_lo, 4) RIO_L(cp_hi, 5)
     RIO_L(cp_seq, 6) RIO_L(p0, 7) RIO_L(p1, 8) RIO_L(p2, 9) RIO_L(qb, 10) RIO_L(pm_ack, 11)
-    RIO_L(pm_hole, 12) RIO_L(pm_win, 13)
+    RIO_L(pm_hole, 12) RIO_L(pm_win, 13) RIO_L(pav_lo, 14) RIO_L(pav_hi, 15) RIO_L(nd_lo, 16)
+    RIO_L(nd_hi, 17) RIO_L(hd_lo, 18) RIO_L(hd_hi, 19)
 #undef RIO_F
 #undef RIO_L
 }
@@ -147,7 +150,7 @@ struct Sim {
     prisma_counters_t* c;
     uint32_t* obs;
     int64_t* wt; uint32_t* wseq;
-    uint4* ring;
+    uint2* ring;
     float* win;
     const int32_t* rowptr; const int32_t* ldst; const int32_t* lrev;
     const int64_t* acctx;
@@ -168,7 +171,7 @@ __device__ inline void sim_bind(Sim& S, const Layout& L, unsigned char* lds, uns
     S.obs = (uint32_t*)(st + L.s_obs);
     S.wt = (int64_t*)(st + L.s_wt);
     S.wseq = (uint32_t*)(st + L.s_wseq);
-    S.ring = (uint4*)(st + L.s_ring);
+    S.ring = (uint2*)(st + L.s_ring);
     S.win = (float*)(st + L.s_win);
     S.rowptr = (const int32_t*)(lds + L.t_rowptr);
     S.ldst = (const int32_t*)(lds + L.t_ldst);
@@ -190,9 +193,9 @@ __device__ __forceinline__ int64_t u_ld64(const int64_t* p) {
     int64_t v = *p;
     return mk64(rfl(lo32(v)), rfl(hi32(v)));
 }
-__device__ __forceinline__ uint4 u_ld128(const uint4* p) {
-    uint4 v = *p;
-    return make_uint4(rfl(v.x), rfl(v.y), rfl(v.z), rfl(v.w));
+__device__ __forceinline__ uint2 u_ld_ent(const uint2* p) {
+    uint2 v = *p;
+    return make_uint2(rfl(v.x), rfl(v.y));
 }
 __device__ __forceinline__ double u_ldd(const double* p) {
     double v = *p;
@@ -307,7 +310,7 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
 
 // returns 1 if enqueued, 0 if dropped (a ring overflow fails the replica)
 template <int FS, int LS>
-__device__ __forceinline__ int link_send(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, uint4 e) {
+__device__ __forceinline__ int link_send(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, uint2 e) {
     const Layout& L = *S.L;
     LinkV k = link_get(R, l);
     uint32_t size = ent_size(L, e.x);
@@ -351,33 +354,31 @@ __device__ __forceinline__ void on_complete(const Sim& S, Regs<FS, LS>& R, Hot& 
 }
 
 // ---- observation (data-packet-manager.cc:171-206)
+// send time in seconds of ping round k as the ping-back manager stores it:
+// (double)GetMilliSeconds() * 0.001 (ping-back-packet-manager.cc:98-116)
+__device__ __forceinline__ double ping_send_s(const Layout& L, int64_t k) {
+    uint64_t ms = (uint64_t)(((k + 1) * L.ping_period) / 1000000);
+    return (double)ms * 0.001;
+}
+
+__device__ __forceinline__ double ld_d(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// 1000 * max(mean(window), min(now - oldest unacknowledged send, 2.6)) for
+// tunnel l.  Acknowledgements of one tunnel arrive in index order, so the
+// oldest pending entry is the first hole below the last ack, else the ping
+// after the last ack if it was sent.  The window mean and both candidate send
+// times are cached per link and refreshed on every ping-back.
 template <int FS, int LS>
-__device__ __forceinline__ uint32_t ping_value(const Sim& S, const Regs<FS, LS>& R, const Hot& H, uint32_t l) {
-    uint32_t pw = R.pm_win.get(l);
-    uint32_t wn = pw & 0xffffu, wh = pw >> 16;
-    double avg = 0.0;
-    if (wn > 0) {
-        double sum = 0.0;
-        uint32_t MA = S.L->ma;
-        uint32_t i = wh;
-        for (uint32_t j = 0; j < wn; ++j) {
-            sum += (double)__uint_as_float(u_ld32((const uint32_t*)S.win + l * MA + i));
-            i = (i + 1 == MA) ? 0 : i + 1;
-        }
-        avg = sum / (double)wn;
-    }
-    // oldest unacknowledged ping (ping-back-packet-manager.cc:110-116):
-    // acknowledgements of one tunnel arrive in index order, so the oldest
-    // pending entry is the first hole below the last ack, else the ping
-    // after the last ack if it was sent.
+__device__ __forceinline__ uint32_t ping_value(const Regs<FS, LS>& R, const Hot& H, uint32_t l, double now_s) {
+    double avg = ld_d(R.pav_lo.get(l), R.pav_hi.get(l));
     int32_t hole = (int32_t)R.pm_hole.get(l), acked = (int32_t)R.pm_ack.get(l);
-    int64_t oldest = -1;
-    if (hole >= 0) oldest = hole;
-    else if ((int64_t)acked + 1 < (int64_t)H.ping_rounds) oldest = (int64_t)acked + 1;
     float mt = 0.0f;
-    if (oldest >= 0) {
-        uint64_t ms = (uint64_t)(((oldest + 1) * S.L->ping_period) / 1000000);
-        double a = ns_to_sec(H.now) - (double)ms * 0.001;
+    bool pend = hole >= 0 || (int64_t)acked + 1 < (int64_t)H.ping_rounds;
+    if (pend) {
+        double od = hole >= 0 ? ld_d(R.hd_lo.get(l), R.hd_hi.get(l)) : ld_d(R.nd_lo.get(l), R.nd_hi.get(l));
+        double a = now_s - od;
         double b = 2.60;
         mt = (float)((b < a) ? b : a);
     }
@@ -388,11 +389,11 @@ __device__ __forceinline__ uint32_t ping_value(const Sim& S, const Regs<FS, LS>&
 // observation words in a per-lane register: lane i holds obs[i]
 template <int FS, int LS>
 __device__ __forceinline__ uint32_t observe(const Sim& S, const Regs<FS, LS>& R, const Hot& H, uint32_t v,
-                                            uint32_t dst) {
+                                            uint32_t dst, double now_s) {
     uint32_t o = (S.lane == 0) ? dst : 0u;
     int r0 = u_ldi(S.rowptr + v), r1 = u_ldi(S.rowptr + v + 1);
     for (int l = r0; l < r1; ++l) {
-        uint32_t val = S.L->ping_as_obs ? ping_value(S, R, H, (uint32_t)l) : R.qb.get((uint32_t)l);
+        uint32_t val = S.L->ping_as_obs ? ping_value(R, H, (uint32_t)l, now_s) : R.qb.get((uint32_t)l);
         o = wrl(o, val, (uint32_t)(1 + l - r0));
     }
     return o;
@@ -409,10 +410,10 @@ __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_
     switch (lane) {
     case 0: hw = lo32(H.now); break;
     case 1: hw = hi32(H.now); break;
-    case 2: hw = (uint32_t)rb; break;
-    case 3: hw = (uint32_t)(rb >> 32); break;
-    case 4: hw = uid; break;
-    case 5: hw = (uint32_t)prev; break;
+    case 2: hw = uid; break;
+    case 3: hw = (uint32_t)prev; break;
+    case 4: hw = (uint32_t)rb; break;
+    case 5: hw = (uint32_t)(rb >> 32); break;
     case 6: hw = node | (dst << 16); break;
     default: hw = w7; break;
     }
@@ -435,15 +436,16 @@ __device__ __forceinline__ void receive_counters(const Sim& S, const Hot& H, uin
     uint32_t type = ent_type(x);
     if (S.lane == 0) {
         prisma_counters_t& c = *S.c;
-        if (type == T_DATA && ent_dst(x) == v) {
+        if (type == T_DATA && d_dst(x) == v) {
             // valable, nextHop == finalDest on identity overlays
             c.ov_arrived++;
-            float cost = (float)(ns_to_sec(H.now) - (double)ent_aux(x));
+            float cost = (float)(ns_to_sec(H.now) - (double)d_start(x));
             c.cost_sum += cost; c.cost_n++;
             c.e2e_sum += cost; c.e2e_n++;
         }
-        if (type > 0 && ent_dst(x) == v) c.bytes_signaling += (int32_t)(L.ping_size - 2);
-        if (type == T_DATA && ent_fresh(x)) {
+        // pings are always addressed to the node that receives them
+        if (type > 0) c.bytes_signaling += (int32_t)(L.ping_size - 2);
+        if (type == T_DATA && d_fresh(x)) {
             c.ov_injected++;
             c.bytes_data += (int32_t)(L.data_size - 2);
         }
@@ -454,19 +456,15 @@ __device__ __forceinline__ void receive_counters(const Sim& S, const Hot& H, uin
 // decision (e, v, d), then the Receive tail.  fused: the record is written
 // here once, with the final status (table policy).
 template <int FS, int LS>
-__device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Hot& H, uint4 e, uint32_t v, uint32_t d,
-                                               int action, bool fused, double reward, int32_t prev,
-                                               uint32_t obs_reg) {
+__device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t x, uint32_t uid,
+                                               uint32_t v, uint32_t d, int action, bool fused, double reward,
+                                               int32_t prev, uint32_t obs_reg) {
     const Layout& L = *S.L;
     int r0 = u_ldi(S.rowptr + v), deg = u_ldi(S.rowptr + v + 1) - r0;
     uint32_t status;
     if (action >= 0 && action < deg) {
         uint32_t l = (uint32_t)(r0 + action);
-        uint4 f;
-        f.x = ent_make(T_DATA, ent_src(e.x), ent_dst(e.x), 0u, 1u, ent_aux(e.x));
-        f.y = e.y;                                   // uid
-        f.z = d;                                     // decision of this hop
-        f.w = (uint32_t)py_micros(H.now);            // temp_obs time
+        uint2 f = make_uint2(d_make(d_dst(x), 0u, d_start(x)), d);   // lastHop = v, prev decision = d
         CNT(S, hops)++;
         CNT(S, hop_deg_sum) += (uint64_t)deg;
         if (link_send(S, R, H, l, f)) {
@@ -483,17 +481,16 @@ __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Ho
     } else {
         status = PRISMA_ST_DISCARDED;
     }
-    if (fused) write_record(S, H, d, reward, e.y, prev, v, ent_dst(e.x), action, status, obs_reg);
+    if (fused) write_record(S, H, d, reward, uid, prev, v, d_dst(x), action, status, obs_reg);
     else patch_record(S, H, d, action, status);
-    receive_counters(S, H, e.x, v);
+    receive_counters(S, H, x, v);
 }
 
 template <int FS, int LS>
 __device__ __forceinline__ void finish_pending(const Sim& S, Regs<FS, LS>& R, Hot& H, int action) {
     const Hdr& h = *S.h;
-    uint4 e = make_uint4(u_ld32(&h.pend_ent[0]), u_ld32(&h.pend_ent[1]), u_ld32(&h.pend_ent[2]),
-                         u_ld32(&h.pend_ent[3]));
-    apply_decision(S, R, H, e, u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action, false, 0.0, 0, 0u);
+    apply_decision(S, R, H, u_ld32(&h.pend_ent[0]), 0u, u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action, false,
+                   0.0, 0, 0u);
     H.pend = 0;
 }
 
@@ -507,11 +504,7 @@ __device__ __forceinline__ void on_ping_round(const Sim& S, Regs<FS, LS>& R, Hot
     for (int u = 0; u < L.N; ++u) {
         int r0 = u_ldi(S.rowptr + u), r1 = u_ldi(S.rowptr + u + 1);
         for (int l = r0; l < r1; ++l) {
-            uint4 e;
-            e.x = ent_make(T_PING_FWD, (uint32_t)u, (uint32_t)u_ldi(S.ldst + l), 0u, 0u, (uint32_t)(l - r0));
-            e.y = k;
-            e.z = ms;
-            e.w = 0;
+            uint2 e = make_uint2(p_make(T_PING_FWD, (uint32_t)(l - r0), k), 0u);
             if (!link_send(S, R, H, (uint32_t)l, e)) CNT(S, ctrl_dropped)++;
         }
         uint32_t s = H.seq++;                                    // re-arm of node u
@@ -544,18 +537,14 @@ __device__ __forceinline__ void on_flow(const Sim& S, Regs<FS, LS>& R, Hot& H, u
     uint32_t draw = R.f_draw.get(f);
     if (draw != 0) {                                                // SendPacket :297-358
         uint32_t src = (uint32_t)u_ldi(S.fsrc + f);
-        uint4 e;
-        e.x = ent_make(T_DATA, src, (uint32_t)u_ldi(S.fdst + f), 1u, 1u, (uint32_t)(H.now / 1000000000));
-        e.y = H.uid++;
-        e.z = 0xffffffffu;
-        e.w = 0;
+        uint2 e = make_uint2(d_make((uint32_t)u_ldi(S.fdst + f), 1u, (uint32_t)(H.now / 1000000000)), H.uid++);
         link_send(S, R, H, (uint32_t)S.L->E + src, e);              // access link
     }
     flow_next(S, R, H, f, draw);                                    // StartSending / ScheduleNextTx
 }
 
 struct Decision {
-    uint4 e; uint32_t v, d; double reward; int32_t prev; uint32_t obs;
+    uint32_t x, uid, v, d; double reward; int32_t prev; uint32_t obs;
 };
 
 // returns 1 if a data decision needs an action
@@ -564,7 +553,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     const Layout& L = *S.L;
     LinkV k = link_get(R, l);
     uint32_t cap = ring_cap(L, l);
-    uint4 e = u_ld128(&S.ring[ring_off(L, l) + k.head]);
+    uint2 e = u_ld_ent(&S.ring[ring_off(L, l) + k.head]);
     k.head = (k.head + 1 == cap) ? 0 : k.head + 1;
     k.n_wire--;
     link_put(S, R, l, k);
@@ -572,43 +561,55 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     uint32_t type = ent_type(e.x);
     if (type == T_DATA) {
         // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
-        uint32_t dst = ent_dst(e.x);
+        uint32_t dst = d_dst(e.x);
         uint32_t d = H.dec++;
+        const double now_s = ns_to_sec(H.now);
         double reward = 0.0;
         int32_t prev = -1;
-        if (!ent_fresh(e.x)) {
-            prev = (int32_t)e.z;
-            reward = py_reward(H.now, e.w);                        // forwarder.py:360
+        uint32_t uid = e.y;
+        if (!d_fresh(e.x)) {
+            // previous decision record (t_ns, uid) from the HBM log: the temp_obs entry
+            // of forwarder.py:153-159
+            prev = (int32_t)e.y;
+            if (d - (uint32_t)prev >= L.log_cap) fail(H, PRISMA_EBIT_LOGWRAP);
+            const uint4 ph = *(const uint4*)(S.logrep + (size_t)((uint32_t)prev & (L.log_cap - 1)) * L.rec_bytes);
+            const int64_t t_prev = mk64(rfl(ph.x), rfl(ph.y));
+            uid = rfl(ph.z);
+            reward = (double)py_micros(H.now) / 1e6 - (double)py_micros(t_prev) / 1e6;   // forwarder.py:360
             CNT(S, reward_sum) += reward;
         }
-        uint32_t o = observe(S, R, H, v, dst);
+        uint32_t o = observe(S, R, H, v, dst, now_s);
         CNT(S, decisions)++;
         if (dst == v) {                                             // getGameOver
-            write_record(S, H, d, reward, e.y, prev, v, dst, -1, PRISMA_ST_DESTINATION, o);
+            write_record(S, H, d, reward, uid, prev, v, dst, -1, PRISMA_ST_DESTINATION, o);
             receive_counters(S, H, e.x, v);
             return 0;
         }
-        if (!fused) write_record(S, H, d, reward, e.y, prev, v, dst, -1, PRISMA_ST_PENDING, o);
-        D.e = e; D.v = v; D.d = d; D.reward = reward; D.prev = prev; D.obs = o;
+        if (!fused) write_record(S, H, d, reward, uid, prev, v, dst, -1, PRISMA_ST_PENDING, o);
+        D.x = e.x; D.uid = uid; D.v = v; D.d = d; D.reward = reward; D.prev = prev; D.obs = o;
         return 1;
     }
     if (type == T_PING_FWD) {                                       // ping-forward-packet-manager.cc:94-156
-        float delay = (float)(ns_to_sec(H.now) - ((double)e.z * 0.001));
-        uint4 b;
-        b.x = ent_make(T_PING_BACK, v, ent_src(e.x), 0u, 0u, ent_aux(e.x));
-        b.y = e.y;
-        b.z = rfl(__float_as_uint(delay));
-        b.w = 0;
+        float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, p_round(e.x)));
+        uint2 b = make_uint2(p_make(T_PING_BACK, p_tunnel(e.x), p_round(e.x)), rfl(__float_as_uint(delay)));
         if (!link_send(S, R, H, (uint32_t)u_ldi(S.lrev + l), b)) CNT(S, ctrl_dropped)++;
     } else if (type == T_PING_BACK) {                               // ping-back-packet-manager.cc:120-144
-        uint32_t lt = (uint32_t)(u_ldi(S.rowptr + v) + (int32_t)ent_aux(e.x));
+        uint32_t lt = (uint32_t)(u_ldi(S.rowptr + v) + (int32_t)p_tunnel(e.x));
         int32_t acked = (int32_t)R.pm_ack.get(lt), hole = (int32_t)R.pm_hole.get(lt);
-        int32_t idx = (int32_t)e.y;
+        int32_t idx = (int32_t)p_round(e.x);
         if (idx <= acked) {
             fail(H, PRISMA_EBIT_ACKORDER);
         } else {
-            if (idx > acked + 1 && hole < 0) R.pm_hole.set(lt, (uint32_t)(acked + 1));
+            if (idx > acked + 1 && hole < 0) {
+                R.pm_hole.set(lt, (uint32_t)(acked + 1));
+                uint64_t hd = __double_as_longlong(ping_send_s(L, acked + 1));
+                R.hd_lo.set(lt, (uint32_t)hd);
+                R.hd_hi.set(lt, (uint32_t)(hd >> 32));
+            }
             R.pm_ack.set(lt, (uint32_t)idx);
+            uint64_t nd = __double_as_longlong(ping_send_s(L, (int64_t)idx + 1));
+            R.nd_lo.set(lt, (uint32_t)nd);
+            R.nd_hi.set(lt, (uint32_t)(nd >> 32));
         }
         uint32_t MA = L.ma;
         uint32_t pw = R.pm_win.get(lt);
@@ -622,7 +623,18 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             wn++;
         }
         R.pm_win.set(lt, wn | (wh << 16));
-        if (S.lane == 0) S.win[lt * MA + slot] = __uint_as_float(e.z);
+        if (S.lane == 0) S.win[lt * MA + slot] = __uint_as_float(e.y);
+        // refresh the cached window mean (data-packet-manager.cc:55-65), summed oldest first
+        double sum = 0.0;
+        uint32_t i = wh;
+        for (uint32_t j = 0; j < wn; ++j) {
+            float w = (i == slot) ? __uint_as_float(e.y) : __uint_as_float(u_ld32((const uint32_t*)S.win + lt * MA + i));
+            sum += (double)w;
+            i = (i + 1 == MA) ? 0 : i + 1;
+        }
+        uint64_t avg = __double_as_longlong(sum / (double)wn);
+        R.pav_lo.set(lt, (uint32_t)avg);
+        R.pav_hi.set(lt, (uint32_t)(avg >> 32));
     }
     receive_counters(S, H, e.x, v);
     return 0;
@@ -661,6 +673,10 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
         R.lk_kind.v[j] = 0; R.cp_lo.v[j] = 0; R.cp_hi.v[j] = 0; R.cp_seq.v[j] = 0;
         R.p0.v[j] = 0; R.p1.v[j] = 0; R.p2.v[j] = 0; R.qb.v[j] = 0;
         R.pm_ack.v[j] = 0xffffffffu; R.pm_hole.v[j] = 0xffffffffu; R.pm_win.v[j] = 0;
+        R.pav_lo.v[j] = 0; R.pav_hi.v[j] = 0;
+        uint64_t nd = __double_as_longlong(ping_send_s(L, 0));
+        R.nd_lo.v[j] = (uint32_t)nd; R.nd_hi.v[j] = (uint32_t)(nd >> 32);
+        R.hd_lo.v[j] = 0; R.hd_hi.v[j] = 0;
     }
     H.now = 0;
     H.ping_t = L.ping_period;                                       // data-packet-manager.cc:118-121
@@ -828,7 +844,7 @@ __global__ void __launch_bounds__(64) prisma_step_kernel_t(KParams P) {
     H.hops_launch = 0;
     if (H.pend && !H.over) {
         if (table_mode) {
-            uint32_t pn = u_ld32(&S.h->pend_node), pd = ent_dst(u_ld32(&S.h->pend_ent[0]));
+            uint32_t pn = u_ld32(&S.h->pend_node), pd = d_dst(u_ld32(&S.h->pend_ent[0]));
             finish_pending(S, R, H, (int)rfl((uint32_t)S.table[pn * NN + pd]));
             H.hops_launch++;
             H.hops_total++;
@@ -863,8 +879,8 @@ __global__ void __launch_bounds__(64) prisma_step_kernel_t(KParams P) {
             Decision D;
             if (on_arrive(S, R, H, id, D, table_mode)) {
                 if (table_mode) {
-                    int a = (int)S.table[D.v * NN + ent_dst(D.e.x)];
-                    apply_decision(S, R, H, D.e, D.v, D.d, (int)rfl((uint32_t)a), true, D.reward, D.prev, D.obs);
+                    int a = (int)S.table[D.v * NN + d_dst(D.x)];
+                    apply_decision(S, R, H, D.x, D.uid, D.v, D.d, (int)rfl((uint32_t)a), true, D.reward, D.prev, D.obs);
                     H.hops_launch++;
                     H.hops_total++;
                     if (H.hops_launch >= max_hops) H.stop = 1;
@@ -872,7 +888,7 @@ __global__ void __launch_bounds__(64) prisma_step_kernel_t(KParams P) {
                     if (lane == 0) {
                         Hdr& h = *S.h;
                         h.pend_link = id; h.pend_node = D.v; h.pend_dec = D.d;
-                        h.pend_ent[0] = D.e.x; h.pend_ent[1] = D.e.y; h.pend_ent[2] = D.e.z; h.pend_ent[3] = D.e.w;
+                        h.pend_ent[0] = D.x; h.pend_ent[1] = D.uid;
                     }
                     if (lane < L.W) S.obs[lane] = D.obs;
                     H.pend = 1;
@@ -987,10 +1003,12 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     if (P->link_bps == 0 || P->link_delay_ns < 0 || P->max_buffer_bytes == 0 || P->packet_size == 0 ||
         P->ma_size == 0 || P->ma_size > 64 || !(P->ping_interval_s > 0.0f))
         return set_err(PRISMA_ERR_CONFIG, "bad link / ping parameters");
-    if (!(P->sim_time_s > 0.0) || P->sim_time_s > 2047.0)
-        return set_err(PRISMA_ERR_CONFIG, "sim_time_s must be in (0, 2047] (11-bit packet start second)");
-    if (P->log_capacity < 64 || (P->log_capacity & (P->log_capacity - 1)))
-        return set_err(PRISMA_ERR_CONFIG, "log_capacity must be a power of two >= 64");
+    if (!(P->sim_time_s > 0.0) || P->sim_time_s > 4095.0)
+        return set_err(PRISMA_ERR_CONFIG, "sim_time_s must be in (0, 4095] (12-bit packet start second)");
+    if (P->sim_time_s / (double)P->ping_interval_s >= (double)(1u << 21))
+        return set_err(PRISMA_ERR_CONFIG, "more than 2^21 ping rounds per episode (21-bit round index)");
+    if (P->log_capacity < 1024 || (P->log_capacity & (P->log_capacity - 1)))
+        return set_err(PRISMA_ERR_CONFIG, "log_capacity must be a power of two >= 1024");
 
     memset(&L, 0, sizeof(L));
     const int Lk = E + N;
@@ -1070,10 +1088,10 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.s_obs = take(4u * L.W);
     L.s_wt = take(8u * Lk * L.WCAP);
     L.s_wseq = take(4u * Lk * L.WCAP);
-    L.s_ring = take(16u * tot);
+    L.s_ring = take(8u * tot);
     L.s_win = take(4u * E * L.MA);
     L.lds_state_bytes = o;
-    L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 14u * 64u * (uint32_t)ls));
+    L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 20u * 64u * (uint32_t)ls));
     L.state_bytes = o;
     L.lds_bytes = L.topo_bytes + L.lds_state_bytes;
     if (L.lds_bytes > 160u * 1024u)

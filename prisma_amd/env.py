@@ -52,7 +52,7 @@ def decode_records(rec: torch.Tensor, W: int) -> dict:
     act = (w7 & 0xFF)
     act = torch.where(act >= 128, act - 256, act)
     return {
-        "t_ns": i64[:, 0], "reward": f64[:, 1], "uid": i32[:, 4], "prev": i32[:, 5],
+        "t_ns": i64[:, 0], "uid": i32[:, 2], "prev": i32[:, 3], "reward": f64[:, 2],
         "node": nd & 0xFFFF, "dst": (nd >> 16) & 0xFFFF, "action": act,
         "status": (w7 >> 8) & 0xFF, "episode": (w7 >> 16) & 0xFFFF, "obs": i32[:, 8:8 + W],
     }

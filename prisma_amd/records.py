@@ -5,7 +5,7 @@ import numpy as np
 
 ST_PENDING, ST_ENQUEUED, ST_DROPPED, ST_DESTINATION, ST_DISCARDED = 0, 1, 2, 3, 4
 
-EBIT_RING, EBIT_WIRE, EBIT_ACKORDER, EBIT_TIME = 1, 2, 4, 8
+EBIT_RING, EBIT_WIRE, EBIT_ACKORDER, EBIT_TIME, EBIT_LOGWRAP = 1, 2, 4, 8, 16
 
 
 def record_dtype(obs_width: int) -> np.dtype:
@@ -13,7 +13,7 @@ def record_dtype(obs_width: int) -> np.dtype:
     if obs_width % 4:
         raise ValueError("obs_width must be a multiple of 4")
     return np.dtype([
-        ("t_ns", "<i8"), ("reward", "<f8"), ("uid", "<u4"), ("prev", "<i4"),
+        ("t_ns", "<i8"), ("uid", "<u4"), ("prev", "<i4"), ("reward", "<f8"),
         ("node", "<u2"), ("dst", "<u2"), ("action", "i1"), ("status", "u1"),
         ("episode", "<u2"), ("obs", "<u4", (obs_width,)),
     ])

@@ -152,8 +152,8 @@ def test_episode_end_and_auto_reset(oracle_mod):
 
 def test_log_ring_wraps(oracle_mod):
     topo = Topology.example("abilene")
-    params = engine_params(topo, sim_time_s=10.0, ping_as_obs=0, log_capacity=64)
-    run_table_both(oracle_mod, topo, params, 3, 1000, sp_next_hop_table(topo))
+    params = engine_params(topo, sim_time_s=30.0, ping_as_obs=0, log_capacity=1024)
+    run_table_both(oracle_mod, topo, params, 3, 6000, sp_next_hop_table(topo))
 
 
 def test_small_topologies_and_single_replica(oracle_mod):
