@@ -42,7 +42,7 @@ using namespace prisma;
 // kernel parameters
 // ---------------------------------------------------------------------------
 struct KParams {
-    Layout lay;
+    const Layout* __restrict__ lay;  // device copy (read through the scalar cache)
     unsigned char* state;        // [R][state_bytes]
     const unsigned char* topo;   // [topo_bytes]
     unsigned char* log;          // [R][log_cap][rec_bytes]
@@ -78,19 +78,22 @@ __device__ __forceinline__ uint32_t hi32(int64_t v) { return (uint32_t)((uint64_
 template <int S>
 struct LA {
     uint32_t v[S];
+    // Every slot is read / compared unconditionally so the slot index never
+    // becomes a dynamic array index (which would demote v[] to scratch).
     __device__ __forceinline__ uint32_t get(uint32_t i) const {
         const uint32_t slot = i >> 6, owner = i & 63u;
-        uint32_t r = 0;
+        uint32_t r = rdl(v[0], owner);
 #pragma unroll
-        for (int j = 0; j < S; ++j)
-            if ((uint32_t)j == slot) r = rdl(v[j], owner);
+        for (int j = 1; j < S; ++j) {
+            const uint32_t t = rdl(v[j], owner);
+            r = (slot == (uint32_t)j) ? t : r;
+        }
         return r;
     }
     __device__ __forceinline__ void set(uint32_t i, uint32_t x) {
-        const uint32_t slot = i >> 6, owner = i & 63u;
 #pragma unroll
         for (int j = 0; j < S; ++j)
-            if ((uint32_t)j == slot) v[j] = wrl(v[j], x, owner);
+            v[j] = (threadIdx.x + 64u * (uint32_t)j == i) ? x : v[j];
     }
     __device__ __forceinline__ void load(const uint32_t* img, int lane) {
 #pragma unroll
@@ -767,7 +770,7 @@ __device__ __forceinline__ void select_event(const Regs<FS, LS>& R, const Hot& H
 // kernels
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void stage_topo(unsigned char* lds, const KParams& P, int lane) {
-    const Layout& L = P.lay;
+    const Layout& L = *P.lay;
     const uint4* t4 = (const uint4*)P.topo;
     uint4* l4 = (uint4*)lds;
     for (uint32_t i = (uint32_t)lane; i < L.topo_bytes / 16u; i += kWave) l4[i] = t4[i];
@@ -780,7 +783,7 @@ __device__ __forceinline__ void stage_topo(unsigned char* lds, const KParams& P,
 
 template <int FS, int LS>
 __device__ __forceinline__ void stage_in(unsigned char* lds, const KParams& P, int r, int lane, Regs<FS, LS>& R) {
-    const Layout& L = P.lay;
+    const Layout& L = *P.lay;
     stage_topo(lds, P, lane);
     const unsigned char* img = P.state + (size_t)r * L.state_bytes;
     const uint4* s4 = (const uint4*)img;
@@ -791,7 +794,7 @@ __device__ __forceinline__ void stage_in(unsigned char* lds, const KParams& P, i
 
 template <int FS, int LS>
 __device__ __forceinline__ void stage_out(unsigned char* lds, const KParams& P, int r, int lane, Regs<FS, LS>& R) {
-    const Layout& L = P.lay;
+    const Layout& L = *P.lay;
     unsigned char* img = P.state + (size_t)r * L.state_bytes;
     uint4* s4 = (uint4*)img;
     const uint4* d4 = (const uint4*)(lds + L.topo_bytes);
@@ -809,7 +812,7 @@ template <int FS, int LS>
 __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
-    const Layout& L = P.lay;
+    const Layout& L = *P.lay;
     stage_topo(lds, P, lane);
     __syncthreads();
     Sim S;
@@ -828,7 +831,7 @@ template <int FS, int LS>
 __global__ void __launch_bounds__(64) prisma_step_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
-    const Layout& L = P.lay;
+    const Layout& L = *P.lay;
     Regs<FS, LS> R;
     stage_in(lds, P, r, lane, R);
     __syncthreads();
@@ -958,6 +961,7 @@ struct prisma_env {
     unsigned char* d_topo = nullptr;
     unsigned char* d_log = nullptr;
     prisma_counters_t* d_cnt = nullptr;
+    Layout* d_lay = nullptr;
     const void* k_step = nullptr;
     const void* k_reset = nullptr;
     bool reset_done = false;
@@ -1136,11 +1140,13 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
     size_t lb = (size_t)L.log_cap * L.rec_bytes * n_replicas;
     if (!HIP_OK(hipMalloc(&e->d_state, sb)) || !HIP_OK(hipMalloc(&e->d_topo, L.topo_bytes)) ||
         !HIP_OK(hipMalloc(&e->d_log, lb)) ||
-        !HIP_OK(hipMalloc((void**)&e->d_cnt, sizeof(prisma_counters_t) * n_replicas))) {
+        !HIP_OK(hipMalloc((void**)&e->d_cnt, sizeof(prisma_counters_t) * n_replicas)) ||
+        !HIP_OK(hipMalloc((void**)&e->d_lay, sizeof(Layout)))) {
         prisma_destroy(e);
         return set_err(PRISMA_ERR_NOMEM, "hipMalloc failed");
     }
     if (!HIP_OK(hipMemcpy(e->d_topo, img.data(), L.topo_bytes, hipMemcpyHostToDevice)) ||
+        !HIP_OK(hipMemcpy(e->d_lay, &L, sizeof(Layout), hipMemcpyHostToDevice)) ||
         !HIP_OK(hipMemset(e->d_log, 0, lb)) ||
         !HIP_OK(hipMemset(e->d_cnt, 0, sizeof(prisma_counters_t) * n_replicas))) {
         prisma_destroy(e);
@@ -1157,7 +1163,7 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
 static KParams base_params(prisma_env_t* e) {
     KParams P;
     memset(&P, 0, sizeof(P));
-    P.lay = e->lay;
+    P.lay = e->d_lay;
     P.state = e->d_state;
     P.topo = e->d_topo;
     P.log = e->d_log;
@@ -1286,5 +1292,6 @@ extern "C" void prisma_destroy(prisma_env_t* e) {
     if (e->d_topo) (void)hipFree(e->d_topo);
     if (e->d_log) (void)hipFree(e->d_log);
     if (e->d_cnt) (void)hipFree(e->d_cnt);
+    if (e->d_lay) (void)hipFree(e->d_lay);
     delete e;
 }
