@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PRISMA_ABI_VERSION 1
+#define PRISMA_ABI_VERSION 2
 
 /* status codes */
 #define PRISMA_OK              0
@@ -136,8 +136,10 @@ typedef struct prisma_record {
     uint32_t uid;
     int32_t  prev;
     double   reward;
-    uint16_t node;
-    uint16_t dst;
+    uint8_t  node;
+    uint8_t  dst;
+    uint16_t start_s;           /* whole second the packet was sent (its
+                                   start-time tag, packet-manager.cc)       */
     int8_t   action;
     uint8_t  status;
     uint16_t episode;

@@ -110,7 +110,7 @@ static double py_reward(int64_t t1, int64_t t0) {
 /* ------------------------------------------------------------------ */
 typedef struct {
     int64_t t_ns; uint32_t uid; int32_t prev; double reward;
-    uint16_t node; uint16_t dst; int8_t action; uint8_t status; uint16_t episode;
+    uint8_t node; uint8_t dst; uint16_t start_s; int8_t action; uint8_t status; uint16_t episode;
 } rec_head_t;
 
 typedef struct {
@@ -599,8 +599,9 @@ static int receive(or_sim_t* s, int di, int p) {
         temp_t* tp = temp_of(s, k->uid);
         r->t_ns = s->now;
         r->uid = k->uid;
-        r->node = (uint16_t)v;
-        r->dst = (uint16_t)k->dst;
+        r->node = (uint8_t)v;
+        r->dst = (uint8_t)k->dst;
+        r->start_s = (uint16_t)k->start_time;
         r->episode = (uint16_t)s->c.episode;
         r->action = -1;
         if (tp->active) {                                             /* handle_transit_packet */

@@ -11,28 +11,32 @@ constexpr int kWave = 64;
 // event kinds in the candidate code (kind << 28 | index)
 constexpr uint32_t K_PING = 0u, K_FLOW = 1u, K_COMPLETE = 2u, K_ARRIVE = 3u;
 
-// packet types (enum-and-constants.h:5-11)
-constexpr uint32_t T_DATA = 0u, T_PING_FWD = 3u, T_PING_BACK = 4u;
-
-// 8-byte packet entry (uint2) of a link ring:
-//   data: x = type(3) | dst(8) << 3 | fresh(1) << 11 | start second(12) << 12
-//         y = decision index of the previous hop (fresh packet: its uid)
-//   ping: x = type(3) | tunnel(8) << 3 | round(21) << 11
-//         y = ping-back one-hop delay (f32 bits)
-// The uid and decision time of a forwarded packet are read back from its
-// previous decision record in the HBM log when it arrives.
-__host__ __device__ inline uint32_t ent_type(uint32_t x) { return x & 7u; }
-__host__ __device__ inline uint32_t d_dst(uint32_t x) { return (x >> 3) & 255u; }
-__host__ __device__ inline uint32_t d_fresh(uint32_t x) { return (x >> 11) & 1u; }
-__host__ __device__ inline uint32_t d_start(uint32_t x) { return x >> 12; }
-__host__ __device__ inline uint32_t p_tunnel(uint32_t x) { return (x >> 3) & 255u; }
-__host__ __device__ inline uint32_t p_round(uint32_t x) { return x >> 11; }
-__host__ __device__ inline uint32_t d_make(uint32_t dst, uint32_t fresh, uint32_t start_s) {
-    return T_DATA | (dst << 3) | (fresh << 11) | (start_s << 12);
+// 4-byte packet entry of a link ring; type in bits 0-1:
+//   T_RELAY  data packet forwarded by a decision: bits 2-31 = that decision's
+//            index mod 2^30 (its uid, destination, start second and decision
+//            time are read back from the decision record in the HBM log)
+//   T_FRESH  data packet of a flow app on its access link: bits 2-10 flow,
+//            bit 11 parity of the start second, bits 12-31 uid mod 2^20
+//   T_PFWD / T_PBACK  ping forward / back (enum-and-constants.h:5-11):
+//            bits 2-8 tunnel, bits 9-31 round; the one-hop delay a ping-back
+//            carries sits in a per-tunnel side table (Layout::s_pbd)
+constexpr uint32_t T_RELAY = 0u, T_FRESH = 1u, T_PFWD = 2u, T_PBACK = 3u;
+__host__ __device__ inline uint32_t ent_type(uint32_t x) { return x & 3u; }
+__host__ __device__ inline bool ent_is_data(uint32_t x) { return (x & 2u) == 0u; }
+__host__ __device__ inline uint32_t r_make(uint32_t dec) { return T_RELAY | (dec << 2); }
+__host__ __device__ inline uint32_t r_dec(uint32_t x) { return x >> 2; }
+__host__ __device__ inline uint32_t f_make(uint32_t flow, uint32_t start_parity, uint32_t uid) {
+    return T_FRESH | (flow << 2) | (start_parity << 11) | (uid << 12);
 }
+__host__ __device__ inline uint32_t f_flow(uint32_t x) { return (x >> 2) & 511u; }
+__host__ __device__ inline uint32_t f_parity(uint32_t x) { return (x >> 11) & 1u; }
+__host__ __device__ inline uint32_t f_uid(uint32_t x) { return x >> 12; }
 __host__ __device__ inline uint32_t p_make(uint32_t type, uint32_t tunnel, uint32_t round) {
-    return type | (tunnel << 3) | (round << 11);
+    return type | (tunnel << 2) | (round << 9);
 }
+__host__ __device__ inline uint32_t p_tunnel(uint32_t x) { return (x >> 2) & 127u; }
+__host__ __device__ inline uint32_t p_round(uint32_t x) { return x >> 9; }
+constexpr uint32_t kRelayMask = (1u << 30) - 1u, kUidMask = (1u << 20) - 1u;
 
 struct Hdr {                 // 128 bytes at state offset 0
     int64_t  now;
@@ -58,32 +62,18 @@ struct Hdr {                 // 128 bytes at state offset 0
 };
 static_assert(sizeof(Hdr) == 128, "Hdr size");
 
-struct LinkState {           // 32 bytes
-    int64_t  complete_t;
-    uint32_t complete_seq;
-    uint32_t q_bytes;        // bytes waiting in the FIFO (excl. the wire)
-    uint16_t head, txp, tail, n_wire;
-    uint16_t n_queue, busy, pad0, pad1;
-};
-static_assert(sizeof(LinkState) == 32, "LinkState size");
-
-struct PingMeta {            // 16 bytes per directed link (= tunnel of its source)
-    int32_t  acked_last;     // highest ping index acknowledged, -1 none
-    int32_t  first_hole;     // lowest never-acknowledged index below acked_last, -1 none
-    uint32_t win_n;
-    uint32_t win_head;
-};
-
-// Offsets (bytes) of every region; filled on the host, passed by value.
+// Offsets (bytes) of every region; filled on the host, read by the kernels
+// from a device copy.
 struct Layout {
     int32_t N, E, L, F, W, max_deg, WCAP, MA;
     uint32_t topo_bytes, state_bytes, lds_bytes, table_bytes;
-    // topology image (LDS offset 0)
-    uint32_t t_rowptr, t_ldst, t_lrev, t_acctx, t_fsrc, t_fdst, t_fmean, t_table;
-    // state image (LDS offset topo_bytes)
-    uint32_t s_hdr, s_cnt, s_obs, s_wt, s_wseq, s_ring, s_win;
+    // topology image (HBM, read through the scalar cache)
+    uint32_t t_rowptr, t_ldst, t_lrev, t_acctx, t_fsrc, t_fdst, t_fmean;
+    // state image (LDS offset 0) and the action table (LDS offset lds_state_bytes)
+    uint32_t s_hdr, s_cnt, s_obs, s_wt, s_wseq, s_ring, s_win, s_pbd;
     uint32_t lds_state_bytes;    // LDS part of the image (bytes [0, lds_state_bytes))
-    uint32_t s_regs;             // register part: 4 x [64*FS] + 14 x [64*LS] u32 arrays
+    uint32_t s_regs;             // register part: 4 x [64*FS] + 20 x [64*LS] u32 arrays
+    uint32_t PBK;                // ping-back delay slots per tunnel (power of two)
     int32_t  FS, LS;             // flow / link register slots per lane
     // link constants (identical on every switch link: sim.cc:414-433)
     int64_t  sw_txd, sw_txp, sw_prop;
@@ -96,7 +86,6 @@ struct Layout {
     uint32_t log_cap, rec_bytes;
     double   loss_penalty;
     float    loss_penalty_f;
-    uint32_t pad;
 };
 
 }  // namespace prisma

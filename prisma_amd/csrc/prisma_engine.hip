@@ -145,45 +145,53 @@ struct Hot {
 // counters live in LDS and are updated by lane 0 only (keeps them out of SGPRs)
 #define CNT(S_, field_) if ((S_).lane == 0) (S_).c->field_
 
-// LDS views of one replica
+// Read-only topology in HBM through the constant address space: every index
+// is wave-uniform, so these become s_load through the scalar cache.
+#define CAS __attribute__((address_space(4)))
+typedef const CAS int32_t c_i32;
+typedef const CAS int64_t c_i64;
+typedef const CAS double c_f64;
+
+// LDS views of one replica + its topology
 struct Sim {
     const Layout* L;
     unsigned char* base;
     Hdr* h;
     prisma_counters_t* c;
     uint32_t* obs;
-    int64_t* wt; uint32_t* wseq;
-    uint2* ring;
+    uint32_t* wt; uint32_t* wseq;           // wire: arrival time (low 32 bits) and seq
+    uint32_t* ring;
     float* win;
-    const int32_t* rowptr; const int32_t* ldst; const int32_t* lrev;
-    const int64_t* acctx;
-    const int32_t* fsrc; const int32_t* fdst; const double* fmean;
+    float* pbd;                             // ping-back delays [E][PBK]
+    c_i32* rowptr; c_i32* ldst; c_i32* lrev;
+    c_i64* acctx;
+    c_i32* fsrc; c_i32* fdst; c_f64* fmean;
     const uint8_t* table;
     unsigned char* logrep;
     uint32_t gid;
     int lane;
 };
 
-__device__ inline void sim_bind(Sim& S, const Layout& L, unsigned char* lds, unsigned char* logrep, uint32_t gid,
-                                int lane) {
+__device__ inline void sim_bind(Sim& S, const Layout& L, unsigned char* lds, const unsigned char* topo,
+                                unsigned char* logrep, uint32_t gid, int lane) {
     S.L = &L;
     S.base = lds;
-    unsigned char* st = lds + L.topo_bytes;
-    S.h = (Hdr*)(st + L.s_hdr);
-    S.c = (prisma_counters_t*)(st + L.s_cnt);
-    S.obs = (uint32_t*)(st + L.s_obs);
-    S.wt = (int64_t*)(st + L.s_wt);
-    S.wseq = (uint32_t*)(st + L.s_wseq);
-    S.ring = (uint2*)(st + L.s_ring);
-    S.win = (float*)(st + L.s_win);
-    S.rowptr = (const int32_t*)(lds + L.t_rowptr);
-    S.ldst = (const int32_t*)(lds + L.t_ldst);
-    S.lrev = (const int32_t*)(lds + L.t_lrev);
-    S.acctx = (const int64_t*)(lds + L.t_acctx);
-    S.fsrc = (const int32_t*)(lds + L.t_fsrc);
-    S.fdst = (const int32_t*)(lds + L.t_fdst);
-    S.fmean = (const double*)(lds + L.t_fmean);
-    S.table = (const uint8_t*)(lds + L.t_table);
+    S.h = (Hdr*)(lds + L.s_hdr);
+    S.c = (prisma_counters_t*)(lds + L.s_cnt);
+    S.obs = (uint32_t*)(lds + L.s_obs);
+    S.wt = (uint32_t*)(lds + L.s_wt);
+    S.wseq = (uint32_t*)(lds + L.s_wseq);
+    S.ring = (uint32_t*)(lds + L.s_ring);
+    S.win = (float*)(lds + L.s_win);
+    S.pbd = (float*)(lds + L.s_pbd);
+    S.rowptr = (c_i32*)(topo + L.t_rowptr);
+    S.ldst = (c_i32*)(topo + L.t_ldst);
+    S.lrev = (c_i32*)(topo + L.t_lrev);
+    S.acctx = (c_i64*)(topo + L.t_acctx);
+    S.fsrc = (c_i32*)(topo + L.t_fsrc);
+    S.fdst = (c_i32*)(topo + L.t_fdst);
+    S.fmean = (c_f64*)(topo + L.t_fmean);
+    S.table = (const uint8_t*)(lds + L.lds_state_bytes);
     S.logrep = logrep;
     S.gid = gid;
     S.lane = lane;
@@ -195,10 +203,6 @@ __device__ __forceinline__ int32_t u_ldi(const int32_t* p) { return (int32_t)rfl
 __device__ __forceinline__ int64_t u_ld64(const int64_t* p) {
     int64_t v = *p;
     return mk64(rfl(lo32(v)), rfl(hi32(v)));
-}
-__device__ __forceinline__ uint2 u_ld_ent(const uint2* p) {
-    uint2 v = *p;
-    return make_uint2(rfl(v.x), rfl(v.y));
 }
 __device__ __forceinline__ double u_ldd(const double* p) {
     double v = *p;
@@ -242,7 +246,7 @@ __device__ __forceinline__ bool key_less(int64_t t, uint32_t s, int64_t bt, uint
 }
 
 __device__ __forceinline__ uint32_t ent_size(const Layout& L, uint32_t x) {
-    return ent_type(x) == T_DATA ? L.data_size : L.ping_size;
+    return ent_is_data(x) ? L.data_size : L.ping_size;
 }
 __device__ __forceinline__ uint32_t ring_off(const Layout& L, uint32_t l) {
     return l < (uint32_t)L.E ? l * L.qcap_s : (uint32_t)L.E * L.qcap_s + (l - (uint32_t)L.E) * L.qcap_a;
@@ -271,7 +275,7 @@ __device__ __forceinline__ LinkV link_get(const Regs<FS, LS>& R, uint32_t l) {
 
 // write back a link's fields and recompute its candidate key
 template <int FS, int LS>
-__device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, uint32_t l, const LinkV& k) {
+__device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, const Hot& H, uint32_t l, const LinkV& k) {
     R.p0.set(l, k.head | (k.txp << 16));
     R.p1.set(l, k.tail | (k.n_wire << 16));
     R.p2.set(l, k.n_queue | (k.busy << 16));
@@ -284,7 +288,7 @@ __device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, uint32_t
     if (k.busy) { t = k.cp_t; s = k.cp_seq; kind = K_COMPLETE; }
     if (k.n_wire) {
         uint32_t w = l * (uint32_t)S.L->WCAP + (k.head & (uint32_t)(S.L->WCAP - 1));
-        int64_t wt = u_ld64(S.wt + w);
+        int64_t wt = H.now + (int64_t)(uint32_t)(u_ld32(S.wt + w) - lo32(H.now));
         uint32_t ws = u_ld32(S.wseq + w);
         if (key_less(wt, ws, t, s)) { t = wt; s = ws; kind = K_ARRIVE; }
     }
@@ -299,7 +303,7 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
                                                uint32_t x) {
     const Layout& L = *S.L;
     const bool sw = l < (uint32_t)L.E;
-    int64_t tx = sw ? (ent_type(x) == T_DATA ? L.sw_txd : L.sw_txp) : u_ld64(S.acctx + (l - (uint32_t)L.E));
+    int64_t tx = sw ? (ent_is_data(x) ? L.sw_txd : L.sw_txp) : S.acctx[l - (uint32_t)L.E];
     int64_t prop = sw ? L.sw_prop : 0;
     k.busy = 1;
     k.cp_t = H.now + tx;
@@ -307,16 +311,16 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
     uint32_t w = l * (uint32_t)L.WCAP + (ring_idx & (uint32_t)(L.WCAP - 1));
     int64_t at = H.now + tx + prop;
     uint32_t as = H.seq++;                                     // channel Receive
-    if (S.lane == 0) { S.wt[w] = at; S.wseq[w] = as; }
+    if (S.lane == 0) { S.wt[w] = lo32(at); S.wseq[w] = as; }
     if (k.n_wire > (uint32_t)L.WCAP) fail(H, PRISMA_EBIT_WIRE);
 }
 
 // returns 1 if enqueued, 0 if dropped (a ring overflow fails the replica)
 template <int FS, int LS>
-__device__ __forceinline__ int link_send(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, uint2 e) {
+__device__ __forceinline__ int link_send(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, uint32_t e) {
     const Layout& L = *S.L;
     LinkV k = link_get(R, l);
-    uint32_t size = ent_size(L, e.x);
+    uint32_t size = ent_size(L, e);
     bool ok = l < (uint32_t)L.E ? (k.qb + size <= L.qmax_bytes) : (k.n_queue + 1u <= L.acc_qmax_pkts);
     if (!ok) return 0;
     uint32_t cap = ring_cap(L, l), off = ring_off(L, l);
@@ -327,14 +331,14 @@ __device__ __forceinline__ int link_send(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     k.qb += size;
     if (!k.busy) {                                              // :643-650
         uint32_t xi = k.txp;
-        uint32_t hx = (k.n_queue == 1) ? e.x : u_ld32(&S.ring[off + xi].x);
+        uint32_t hx = (k.n_queue == 1) ? e : u_ld32(&S.ring[off + xi]);
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
         k.qb -= ent_size(L, hx);
         transmit_start(S, H, l, k, xi, hx);
     }
-    link_put(S, R, l, k);
+    link_put(S, R, H, l, k);
     return 1;
 }
 
@@ -346,14 +350,14 @@ __device__ __forceinline__ void on_complete(const Sim& S, Regs<FS, LS>& R, Hot& 
     if (k.n_queue) {
         uint32_t cap = ring_cap(L, l);
         uint32_t xi = k.txp;
-        uint32_t hx = u_ld32(&S.ring[ring_off(L, l) + xi].x);
+        uint32_t hx = u_ld32(&S.ring[ring_off(L, l) + xi]);
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
         k.qb -= ent_size(L, hx);
         transmit_start(S, H, l, k, xi, hx);
     }
-    link_put(S, R, l, k);
+    link_put(S, R, H, l, k);
 }
 
 // ---- observation (data-packet-manager.cc:171-206)
@@ -394,7 +398,7 @@ template <int FS, int LS>
 __device__ __forceinline__ uint32_t observe(const Sim& S, const Regs<FS, LS>& R, const Hot& H, uint32_t v,
                                             uint32_t dst, double now_s) {
     uint32_t o = (S.lane == 0) ? dst : 0u;
-    int r0 = u_ldi(S.rowptr + v), r1 = u_ldi(S.rowptr + v + 1);
+    int r0 = S.rowptr[v], r1 = S.rowptr[v + 1];
     for (int l = r0; l < r1; ++l) {
         uint32_t val = S.L->ping_as_obs ? ping_value(R, H, (uint32_t)l, now_s) : R.qb.get((uint32_t)l);
         o = wrl(o, val, (uint32_t)(1 + l - r0));
@@ -404,8 +408,8 @@ __device__ __forceinline__ uint32_t observe(const Sim& S, const Regs<FS, LS>& R,
 
 // one coalesced wave store of a decision record (lane i writes word i)
 __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_t d, double reward, uint32_t uid,
-                                             int32_t prev, uint32_t node, uint32_t dst, int action, uint32_t status,
-                                             uint32_t obs_reg) {
+                                             int32_t prev, uint32_t node, uint32_t dst, uint32_t start, int action,
+                                             uint32_t status, uint32_t obs_reg) {
     const int lane = S.lane;
     uint64_t rb = __double_as_longlong(reward);
     uint32_t w7 = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
@@ -417,7 +421,7 @@ __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_
     case 3: hw = (uint32_t)prev; break;
     case 4: hw = (uint32_t)rb; break;
     case 5: hw = (uint32_t)(rb >> 32); break;
-    case 6: hw = node | (dst << 16); break;
+    case 6: hw = node | (dst << 8) | (start << 16); break;
     default: hw = w7; break;
     }
     uint32_t ob = (uint32_t)__shfl((int)obs_reg, (lane - 8) & 63);
@@ -433,44 +437,44 @@ __device__ __forceinline__ void patch_record(const Sim& S, const Hot& H, uint32_
     }
 }
 
-// Receive tail after the MacRx trace (point-to-point-net-device.cc:430-463)
-__device__ __forceinline__ void receive_counters(const Sim& S, const Hot& H, uint32_t x, uint32_t v) {
+// Receive tail after the MacRx trace (point-to-point-net-device.cc:430-463).
+// arrived: a data packet at its destination (start = its start second).
+__device__ __forceinline__ void receive_counters(const Sim& S, const Hot& H, uint32_t x, bool arrived, uint32_t start) {
     const Layout& L = *S.L;
-    uint32_t type = ent_type(x);
     if (S.lane == 0) {
         prisma_counters_t& c = *S.c;
-        if (type == T_DATA && d_dst(x) == v) {
+        if (arrived) {
             // valable, nextHop == finalDest on identity overlays
             c.ov_arrived++;
-            float cost = (float)(ns_to_sec(H.now) - (double)d_start(x));
+            float cost = (float)(ns_to_sec(H.now) - (double)start);
             c.cost_sum += cost; c.cost_n++;
             c.e2e_sum += cost; c.e2e_n++;
         }
         // pings are always addressed to the node that receives them
-        if (type > 0) c.bytes_signaling += (int32_t)(L.ping_size - 2);
-        if (type == T_DATA && d_fresh(x)) {
+        if (!ent_is_data(x)) c.bytes_signaling += (int32_t)(L.ping_size - 2);
+        if (ent_type(x) == T_FRESH) {
             c.ov_injected++;
             c.bytes_data += (int32_t)(L.data_size - 2);
         }
     }
 }
 
-// DataPacketManager::sendPacket (data-packet-manager.cc:251-299) for the
-// decision (e, v, d), then the Receive tail.  fused: the record is written
-// here once, with the final status (table policy).
+// DataPacketManager::sendPacket (data-packet-manager.cc:251-299) for decision
+// d at node v, then the Receive tail.  x is the arriving entry (for the
+// counters); fused: the record is written here once, with the final status
+// (table policy).
 template <int FS, int LS>
-__device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t x, uint32_t uid,
-                                               uint32_t v, uint32_t d, int action, bool fused, double reward,
-                                               int32_t prev, uint32_t obs_reg) {
+__device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t x, uint32_t dst,
+                                               uint32_t start, uint32_t uid, uint32_t v, uint32_t d, int action,
+                                               bool fused, double reward, int32_t prev, uint32_t obs_reg) {
     const Layout& L = *S.L;
-    int r0 = u_ldi(S.rowptr + v), deg = u_ldi(S.rowptr + v + 1) - r0;
+    int r0 = S.rowptr[v], deg = S.rowptr[v + 1] - r0;
     uint32_t status;
     if (action >= 0 && action < deg) {
         uint32_t l = (uint32_t)(r0 + action);
-        uint2 f = make_uint2(d_make(d_dst(x), 0u, d_start(x)), d);   // lastHop = v, prev decision = d
         CNT(S, hops)++;
         CNT(S, hop_deg_sum) += (uint64_t)deg;
-        if (link_send(S, R, H, l, f)) {
+        if (link_send(S, R, H, l, r_make(d))) {                   // lastHop = v, previous decision = d
             status = PRISMA_ST_ENQUEUED;
         } else {
             status = PRISMA_ST_DROPPED;              // :655-664 + forwarder.py:214-244
@@ -484,16 +488,16 @@ __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Ho
     } else {
         status = PRISMA_ST_DISCARDED;
     }
-    if (fused) write_record(S, H, d, reward, uid, prev, v, d_dst(x), action, status, obs_reg);
+    if (fused) write_record(S, H, d, reward, uid, prev, v, dst, start, action, status, obs_reg);
     else patch_record(S, H, d, action, status);
-    receive_counters(S, H, x, v);
+    receive_counters(S, H, x, false, 0u);
 }
 
 template <int FS, int LS>
 __device__ __forceinline__ void finish_pending(const Sim& S, Regs<FS, LS>& R, Hot& H, int action) {
     const Hdr& h = *S.h;
-    apply_decision(S, R, H, u_ld32(&h.pend_ent[0]), 0u, u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action, false,
-                   0.0, 0, 0u);
+    apply_decision(S, R, H, u_ld32(&h.pend_ent[0]), 0u, 0u, 0u, u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action,
+                   false, 0.0, 0, 0u);
     H.pend = 0;
 }
 
@@ -502,13 +506,11 @@ template <int FS, int LS>
 __device__ __forceinline__ void on_ping_round(const Sim& S, Regs<FS, LS>& R, Hot& H) {   // data-packet-manager.cc:350-413
     const Layout& L = *S.L;
     uint32_t k = H.ping_rounds;
-    uint32_t ms = (uint32_t)(H.now / 1000000);
     uint32_t first_rearm = 0;
     for (int u = 0; u < L.N; ++u) {
-        int r0 = u_ldi(S.rowptr + u), r1 = u_ldi(S.rowptr + u + 1);
+        int r0 = S.rowptr[u], r1 = S.rowptr[u + 1];
         for (int l = r0; l < r1; ++l) {
-            uint2 e = make_uint2(p_make(T_PING_FWD, (uint32_t)(l - r0), k), 0u);
-            if (!link_send(S, R, H, (uint32_t)l, e)) CNT(S, ctrl_dropped)++;
+            if (!link_send(S, R, H, (uint32_t)l, p_make(T_PFWD, (uint32_t)(l - r0), k))) CNT(S, ctrl_dropped)++;
         }
         uint32_t s = H.seq++;                                    // re-arm of node u
         if (u == 0) first_rearm = s;
@@ -527,7 +529,7 @@ __device__ __forceinline__ void flow_next(const Sim& S, Regs<FS, LS>& R, Hot& H,
     philox4x32_10(c, S.L->seed_lo, S.gid);
     uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
     double U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
-    double delay = -u_ldd(S.fmean + f) * det_log(U);
+    double delay = -S.fmean[f] * det_log(U);
     int64_t t = H.now + sec_to_ns(delay);
     R.fk_lo.set(f, lo32(t));
     R.fk_hi.set(f, hi32(t));
@@ -539,15 +541,16 @@ template <int FS, int LS>
 __device__ __forceinline__ void on_flow(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t f) {
     uint32_t draw = R.f_draw.get(f);
     if (draw != 0) {                                                // SendPacket :297-358
-        uint32_t src = (uint32_t)u_ldi(S.fsrc + f);
-        uint2 e = make_uint2(d_make((uint32_t)u_ldi(S.fdst + f), 1u, (uint32_t)(H.now / 1000000000)), H.uid++);
-        link_send(S, R, H, (uint32_t)S.L->E + src, e);              // access link
+        uint32_t src = (uint32_t)S.fsrc[f];
+        uint32_t par = (uint32_t)(H.now / 1000000000) & 1u;         // start second (its parity)
+        link_send(S, R, H, (uint32_t)S.L->E + src, f_make(f, par, H.uid & kUidMask));   // access link
+        H.uid++;
     }
     flow_next(S, R, H, f, draw);                                    // StartSending / ScheduleNextTx
 }
 
 struct Decision {
-    uint32_t x, uid, v, d; double reward; int32_t prev; uint32_t obs;
+    uint32_t x, dst, start, uid, v, d; double reward; int32_t prev; uint32_t obs;
 };
 
 // returns 1 if a data decision needs an action
@@ -556,50 +559,66 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     const Layout& L = *S.L;
     LinkV k = link_get(R, l);
     uint32_t cap = ring_cap(L, l);
-    uint2 e = u_ld_ent(&S.ring[ring_off(L, l) + k.head]);
+    const uint32_t x = u_ld32(&S.ring[ring_off(L, l) + k.head]);
     k.head = (k.head + 1 == cap) ? 0 : k.head + 1;
     k.n_wire--;
-    link_put(S, R, l, k);
-    uint32_t v = (uint32_t)u_ldi(S.ldst + l);
-    uint32_t type = ent_type(e.x);
-    if (type == T_DATA) {
+    link_put(S, R, H, l, k);
+    const uint32_t v = (uint32_t)S.ldst[l];
+    const uint32_t type = ent_type(x);
+    if (ent_is_data(x)) {
         // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
-        uint32_t dst = d_dst(e.x);
-        uint32_t d = H.dec++;
-        const double now_s = ns_to_sec(H.now);
+        const uint32_t d = H.dec++;
         double reward = 0.0;
         int32_t prev = -1;
-        uint32_t uid = e.y;
-        if (!d_fresh(e.x)) {
-            // previous decision record (t_ns, uid) from the HBM log: the temp_obs entry
-            // of forwarder.py:153-159
-            prev = (int32_t)e.y;
-            if (d - (uint32_t)prev >= L.log_cap) fail(H, PRISMA_EBIT_LOGWRAP);
-            const uint4 ph = *(const uint4*)(S.logrep + (size_t)((uint32_t)prev & (L.log_cap - 1)) * L.rec_bytes);
+        uint32_t dst, start, uid;
+        if (type == T_FRESH) {
+            // first notification: destination from the flow, uid and start
+            // second rebuilt from their low bits (the packet left its app less
+            // than 1 s and fewer than 2^20 injections ago)
+            const uint32_t f = f_flow(x);
+            dst = (uint32_t)S.fdst[f];
+            const uint32_t s0 = (uint32_t)(H.now / 1000000000);
+            start = s0 - ((s0 ^ f_parity(x)) & 1u);
+            const uint32_t last = H.uid - 1u;
+            uid = last - ((last - f_uid(x)) & kUidMask);
+        } else {
+            // previous decision record (t_ns, uid, dst, start) from the HBM
+            // log: the temp_obs entry of forwarder.py:153-159
+            const uint32_t dist = (d - r_dec(x)) & kRelayMask;
+            prev = (int32_t)(d - dist);
+            if (dist >= L.log_cap) fail(H, PRISMA_EBIT_LOGWRAP);
+            const unsigned char* pr = S.logrep + (size_t)((uint32_t)prev & (L.log_cap - 1)) * L.rec_bytes;
+            const uint4 ph = *(const uint4*)pr;
+            const uint32_t w6 = rfl(*(const uint32_t*)(pr + 24));
             const int64_t t_prev = mk64(rfl(ph.x), rfl(ph.y));
             uid = rfl(ph.z);
+            dst = (w6 >> 8) & 255u;
+            start = w6 >> 16;
             reward = (double)py_micros(H.now) / 1e6 - (double)py_micros(t_prev) / 1e6;   // forwarder.py:360
             CNT(S, reward_sum) += reward;
         }
-        uint32_t o = observe(S, R, H, v, dst, now_s);
+        uint32_t o = observe(S, R, H, v, dst, ns_to_sec(H.now));
         CNT(S, decisions)++;
         if (dst == v) {                                             // getGameOver
-            write_record(S, H, d, reward, uid, prev, v, dst, -1, PRISMA_ST_DESTINATION, o);
-            receive_counters(S, H, e.x, v);
+            write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_DESTINATION, o);
+            receive_counters(S, H, x, true, start);
             return 0;
         }
-        if (!fused) write_record(S, H, d, reward, uid, prev, v, dst, -1, PRISMA_ST_PENDING, o);
-        D.x = e.x; D.uid = uid; D.v = v; D.d = d; D.reward = reward; D.prev = prev; D.obs = o;
+        if (!fused) write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_PENDING, o);
+        D.x = x; D.dst = dst; D.start = start; D.uid = uid; D.v = v; D.d = d; D.reward = reward; D.prev = prev;
+        D.obs = o;
         return 1;
     }
-    if (type == T_PING_FWD) {                                       // ping-forward-packet-manager.cc:94-156
-        float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, p_round(e.x)));
-        uint2 b = make_uint2(p_make(T_PING_BACK, p_tunnel(e.x), p_round(e.x)), rfl(__float_as_uint(delay)));
-        if (!link_send(S, R, H, (uint32_t)u_ldi(S.lrev + l), b)) CNT(S, ctrl_dropped)++;
-    } else if (type == T_PING_BACK) {                               // ping-back-packet-manager.cc:120-144
-        uint32_t lt = (uint32_t)(u_ldi(S.rowptr + v) + (int32_t)p_tunnel(e.x));
+    const uint32_t tun = p_tunnel(x), rnd = p_round(x);
+    if (type == T_PFWD) {                                           // ping-forward-packet-manager.cc:94-156
+        float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
+        if (S.lane == 0) S.pbd[l * L.PBK + (rnd & (L.PBK - 1))] = delay;
+        if (!link_send(S, R, H, (uint32_t)S.lrev[l], p_make(T_PBACK, tun, rnd))) CNT(S, ctrl_dropped)++;
+    } else {                                                        // ping-back-packet-manager.cc:120-144
+        const uint32_t lt = (uint32_t)S.rowptr[v] + tun;
+        const float delay = __uint_as_float(u_ld32((const uint32_t*)S.pbd + lt * L.PBK + (rnd & (L.PBK - 1))));
         int32_t acked = (int32_t)R.pm_ack.get(lt), hole = (int32_t)R.pm_hole.get(lt);
-        int32_t idx = (int32_t)p_round(e.x);
+        int32_t idx = (int32_t)rnd;
         if (idx <= acked) {
             fail(H, PRISMA_EBIT_ACKORDER);
         } else {
@@ -626,12 +645,12 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             wn++;
         }
         R.pm_win.set(lt, wn | (wh << 16));
-        if (S.lane == 0) S.win[lt * MA + slot] = __uint_as_float(e.y);
+        if (S.lane == 0) S.win[lt * MA + slot] = delay;
         // refresh the cached window mean (data-packet-manager.cc:55-65), summed oldest first
         double sum = 0.0;
         uint32_t i = wh;
         for (uint32_t j = 0; j < wn; ++j) {
-            float w = (i == slot) ? __uint_as_float(e.y) : __uint_as_float(u_ld32((const uint32_t*)S.win + lt * MA + i));
+            float w = (i == slot) ? delay : __uint_as_float(u_ld32((const uint32_t*)S.win + lt * MA + i));
             sum += (double)w;
             i = (i + 1 == MA) ? 0 : i + 1;
         }
@@ -639,7 +658,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
         R.pav_lo.set(lt, (uint32_t)avg);
         R.pav_hi.set(lt, (uint32_t)(avg >> 32));
     }
-    receive_counters(S, H, e.x, v);
+    receive_counters(S, H, x, false, 0u);
     return 0;
 }
 
@@ -653,7 +672,7 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
     uint32_t dec = H.dec, hl = H.hops_launch;
     uint64_t ht = H.hops_total, et = H.events_total;
     __syncthreads();
-    uint4* st4 = (uint4*)(S.base + L.topo_bytes);
+    uint4* st4 = (uint4*)S.base;
     for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < FS; ++j) {
@@ -769,13 +788,11 @@ __device__ __forceinline__ void select_event(const Regs<FS, LS>& R, const Hot& H
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void stage_topo(unsigned char* lds, const KParams& P, int lane) {
+// the [N][N] action table (table policy) sits in LDS after the state image
+__device__ __forceinline__ void stage_table(unsigned char* lds, const KParams& P, int lane) {
     const Layout& L = *P.lay;
-    const uint4* t4 = (const uint4*)P.topo;
-    uint4* l4 = (uint4*)lds;
-    for (uint32_t i = (uint32_t)lane; i < L.topo_bytes / 16u; i += kWave) l4[i] = t4[i];
-    if (P.table && L.table_bytes) {
-        uint8_t* dstp = lds + L.t_table;
+    if (P.table) {
+        uint8_t* dstp = lds + L.lds_state_bytes;
         const uint32_t nt = (uint32_t)(L.N * L.N);
         for (uint32_t i = (uint32_t)lane; i < nt; i += kWave) dstp[i] = P.table[i];
     }
@@ -784,10 +801,10 @@ __device__ __forceinline__ void stage_topo(unsigned char* lds, const KParams& P,
 template <int FS, int LS>
 __device__ __forceinline__ void stage_in(unsigned char* lds, const KParams& P, int r, int lane, Regs<FS, LS>& R) {
     const Layout& L = *P.lay;
-    stage_topo(lds, P, lane);
+    stage_table(lds, P, lane);
     const unsigned char* img = P.state + (size_t)r * L.state_bytes;
     const uint4* s4 = (const uint4*)img;
-    uint4* d4 = (uint4*)(lds + L.topo_bytes);
+    uint4* d4 = (uint4*)lds;
     for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes / 16u; i += kWave) d4[i] = s4[i];
     regs_io(R, (uint32_t*)(const_cast<unsigned char*>(img) + L.s_regs), lane, false);
 }
@@ -797,7 +814,7 @@ __device__ __forceinline__ void stage_out(unsigned char* lds, const KParams& P, 
     const Layout& L = *P.lay;
     unsigned char* img = P.state + (size_t)r * L.state_bytes;
     uint4* s4 = (uint4*)img;
-    const uint4* d4 = (const uint4*)(lds + L.topo_bytes);
+    const uint4* d4 = (const uint4*)lds;
     for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes / 16u; i += kWave) s4[i] = d4[i];
     regs_io(R, (uint32_t*)(img + L.s_regs), lane, true);
 }
@@ -813,10 +830,8 @@ __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
     const Layout& L = *P.lay;
-    stage_topo(lds, P, lane);
-    __syncthreads();
     Sim S;
-    sim_bind(S, L, lds, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r, lane);
+    sim_bind(S, L, lds, P.topo, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r, lane);
     Regs<FS, LS> R;
     Hot H;
     memset(&H, 0, sizeof(H));
@@ -836,7 +851,7 @@ __global__ void __launch_bounds__(64) prisma_step_kernel_t(KParams P) {
     stage_in(lds, P, r, lane, R);
     __syncthreads();
     Sim S;
-    sim_bind(S, L, lds, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r, lane);
+    sim_bind(S, L, lds, P.topo, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r, lane);
     const bool table_mode = (P.mode == 2);
     const uint32_t max_hops = (uint32_t)P.max_hops;
     const uint32_t NN = (uint32_t)L.N;
@@ -847,7 +862,7 @@ __global__ void __launch_bounds__(64) prisma_step_kernel_t(KParams P) {
     H.hops_launch = 0;
     if (H.pend && !H.over) {
         if (table_mode) {
-            uint32_t pn = u_ld32(&S.h->pend_node), pd = d_dst(u_ld32(&S.h->pend_ent[0]));
+            uint32_t pn = u_ld32(&S.h->pend_node), pd = u_ld32(&S.h->pend_ent[1]);
             finish_pending(S, R, H, (int)rfl((uint32_t)S.table[pn * NN + pd]));
             H.hops_launch++;
             H.hops_total++;
@@ -882,8 +897,9 @@ __global__ void __launch_bounds__(64) prisma_step_kernel_t(KParams P) {
             Decision D;
             if (on_arrive(S, R, H, id, D, table_mode)) {
                 if (table_mode) {
-                    int a = (int)S.table[D.v * NN + d_dst(D.x)];
-                    apply_decision(S, R, H, D.x, D.uid, D.v, D.d, (int)rfl((uint32_t)a), true, D.reward, D.prev, D.obs);
+                    int a = (int)S.table[D.v * NN + D.dst];
+                    apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, (int)rfl((uint32_t)a), true,
+                                   D.reward, D.prev, D.obs);
                     H.hops_launch++;
                     H.hops_total++;
                     if (H.hops_launch >= max_hops) H.stop = 1;
@@ -891,7 +907,7 @@ __global__ void __launch_bounds__(64) prisma_step_kernel_t(KParams P) {
                     if (lane == 0) {
                         Hdr& h = *S.h;
                         h.pend_link = id; h.pend_node = D.v; h.pend_dec = D.d;
-                        h.pend_ent[0] = D.x; h.pend_ent[1] = D.uid;
+                        h.pend_ent[0] = D.x; h.pend_ent[1] = D.dst;
                     }
                     if (lane < L.W) S.obs[lane] = D.obs;
                     H.pend = 1;
@@ -1053,6 +1069,15 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.qcap_s = qs;
     L.qcap_a = (uint32_t)(L.WCAP < 8 ? 8 : L.WCAP);
     uint32_t tot = (uint32_t)E * L.qcap_s + (uint32_t)N * L.qcap_a;
+    // ping-back delay slots per tunnel: round k's slot is reused by round
+    // k + PBK, whose forward ping arrives after round k's ping-back (at most
+    // span after k's send) has been consumed
+    L.PBK = next_pow2((uint32_t)(span / (double)P->ping_interval_s) + 2u);
+    // wire arrival times are kept as their low 32 bits relative to the clock
+    int64_t max_acc = 0;
+    for (int u = 0; u < N; ++u) max_acc = acctx[u] > max_acc ? acctx[u] : max_acc;
+    if ((L.sw_txd > max_acc ? L.sw_txd : max_acc) + L.sw_prop >= ((int64_t)1 << 31))
+        return set_err(PRISMA_ERR_CONFIG, "transmission + propagation delay above 2^31 ns");
 
     // topology image
     uint32_t o = 0;
@@ -1064,7 +1089,6 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.t_fsrc = take(4u * F);
     L.t_fdst = take(4u * F);
     L.t_fmean = take(8u * F);
-    L.t_table = take((uint32_t)(N * N));
     L.table_bytes = (uint32_t)(N * N);
     L.topo_bytes = o;
     topo.assign(o, 0);
@@ -1090,14 +1114,15 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.s_hdr = take(sizeof(Hdr));
     L.s_cnt = take(sizeof(prisma_counters_t));
     L.s_obs = take(4u * L.W);
-    L.s_wt = take(8u * Lk * L.WCAP);
+    L.s_wt = take(4u * Lk * L.WCAP);
     L.s_wseq = take(4u * Lk * L.WCAP);
-    L.s_ring = take(8u * tot);
+    L.s_ring = take(4u * tot);
     L.s_win = take(4u * E * L.MA);
+    L.s_pbd = take(4u * E * L.PBK);
     L.lds_state_bytes = o;
     L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 20u * 64u * (uint32_t)ls));
     L.state_bytes = o;
-    L.lds_bytes = L.topo_bytes + L.lds_state_bytes;
+    L.lds_bytes = L.lds_state_bytes + align16(L.table_bytes);
     if (L.lds_bytes > 160u * 1024u)
         return set_err(PRISMA_ERR_CONFIG, "replica state exceeds the 160 KiB LDS of a gfx950 CU");
 

@@ -90,7 +90,7 @@ def load_library(path: str = LIB_PATH):
     L.prisma_state_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.prisma_destroy.restype = None
     L.prisma_destroy.argtypes = [C.c_void_p]
-    if L.prisma_abi_version() != 1:
+    if L.prisma_abi_version() != 2:
         raise PrismaError("libprisma_amd ABI version mismatch")
     _lib = L
     return L

@@ -14,7 +14,7 @@ def record_dtype(obs_width: int) -> np.dtype:
         raise ValueError("obs_width must be a multiple of 4")
     return np.dtype([
         ("t_ns", "<i8"), ("uid", "<u4"), ("prev", "<i4"), ("reward", "<f8"),
-        ("node", "<u2"), ("dst", "<u2"), ("action", "i1"), ("status", "u1"),
+        ("node", "u1"), ("dst", "u1"), ("start_s", "<u2"), ("action", "i1"), ("status", "u1"),
         ("episode", "<u2"), ("obs", "<u4", (obs_width,)),
     ])
 
