@@ -28,7 +28,8 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-METRIC = "packet-hop transitions/sec at 4096 Abilene replicas; achieved HBM GB/s"
+METRIC = "packet-hop transitions/sec at 4096 Abilene replicas; achieved HBM GB/s"   # BASELINE.json
+KERNEL_SOURCES = ["prisma_amd/csrc/prisma_engine.hip", "prisma_amd/csrc/engine_layout.h", "prisma_amd/csrc/numerics.h"]
 HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
@@ -80,13 +81,24 @@ def cpu_baseline(topo, params, table, hops_per_replica: int):
                       f"one replica per host thread, {dt:.2f} s wall; ns-3 reference path not runnable (SURVEY 8c)"}
 
 
-def pmc_traffic(replicas: int, hops: int):
-    """HBM bytes per launch from the committed rocprofv3 --pmc passes (profiles/pmc_traffic.json)."""
+def kernel_source_hash() -> str:
+    import hashlib
+    h = hashlib.sha1()
+    for f in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
+def pmc_traffic(topology: str, replicas: int, hops: int):
+    """HBM bytes per launch from the committed rocprofv3 --pmc passes (profiles/pmc_traffic.json),
+    used only when they were collected on this workload with this exact kernel source."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as fh:
             d = json.load(fh)
-        if int(d.get("replicas", -1)) == replicas and int(d.get("hops", -1)) == hops:
+        if (d.get("topology") == topology and int(d.get("replicas", -1)) == replicas
+                and int(d.get("hops", -1)) == hops and d.get("kernel_source") == kernel_source_hash()):
             return float(d["bytes_per_launch"])
     except (OSError, ValueError, KeyError):
         pass
@@ -170,9 +182,11 @@ def main():
         hops_per_launch = hops_local / args.steps
         alg_bytes = algorithmic_bytes(int(round(hops_per_launch)), int(round(hops_per_launch * deg_avg)))
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(args.replicas, args.hops)
+        traffic = pmc_traffic(args.topology, args.replicas, args.hops)
+        metric = METRIC if (args.topology, args.replicas) == ("abilene", 4096) else \
+            f"packet-hop transitions/sec at {args.replicas} {topo.name} replicas; achieved HBM GB/s"
         result = {
-            "metric": METRIC,
+            "metric": metric,
             "value": hops_total / elapsed,
             "unit": "hops/s",
             "n_gpus": world,
@@ -183,7 +197,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic (Poisson traffic from the shipped Abilene TM0; random-init DQ-routing weights)",
+            "data": f"synthetic (Poisson traffic from the shipped {topo.name} TM{args.tm} x load_factor "
+                    f"{args.load_factor}; random-init DQ-routing weights)",
             "config": {
                 "workload": f"{args.topology} tm{args.tm} lf{args.load_factor} dq_routing greedy, "
                             f"{args.replicas} replicas/GPU x {args.hops} hops/step, pingAsObs={args.ping_as_obs}, "
@@ -195,7 +210,7 @@ def main():
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "prisma_step_kernel", "kernel_ms": kern_ms,
+                "kernel": eng.kernel_name, "kernel_ms": kern_ms, "kernel_source": kernel_source_hash(),
                 "alg_bytes_per_launch": alg_bytes, "hops_per_launch": hops_per_launch,
             },
             "errors": errors,

@@ -151,10 +151,11 @@ struct Hot {
 typedef const CAS int32_t c_i32;
 typedef const CAS int64_t c_i64;
 typedef const CAS double c_f64;
+typedef const CAS Layout CLayout;        // scenario constants: s_load, never clobbered
 
 // LDS views of one replica + its topology
 struct Sim {
-    const Layout* L;
+    CLayout* L;
     unsigned char* base;
     Hdr* h;
     prisma_counters_t* c;
@@ -172,7 +173,7 @@ struct Sim {
     int lane;
 };
 
-__device__ inline void sim_bind(Sim& S, const Layout& L, unsigned char* lds, const unsigned char* topo,
+__device__ inline void sim_bind(Sim& S, CLayout& L, unsigned char* lds, const unsigned char* topo,
                                 unsigned char* logrep, uint32_t gid, int lane) {
     S.L = &L;
     S.base = lds;
@@ -245,13 +246,13 @@ __device__ __forceinline__ bool key_less(int64_t t, uint32_t s, int64_t bt, uint
     return t < bt || (t == bt && s < bs);
 }
 
-__device__ __forceinline__ uint32_t ent_size(const Layout& L, uint32_t x) {
+__device__ __forceinline__ uint32_t ent_size(CLayout& L, uint32_t x) {
     return ent_is_data(x) ? L.data_size : L.ping_size;
 }
-__device__ __forceinline__ uint32_t ring_off(const Layout& L, uint32_t l) {
+__device__ __forceinline__ uint32_t ring_off(CLayout& L, uint32_t l) {
     return l < (uint32_t)L.E ? l * L.qcap_s : (uint32_t)L.E * L.qcap_s + (l - (uint32_t)L.E) * L.qcap_a;
 }
-__device__ __forceinline__ uint32_t ring_cap(const Layout& L, uint32_t l) { return l < (uint32_t)L.E ? L.qcap_s : L.qcap_a; }
+__device__ __forceinline__ uint32_t ring_cap(CLayout& L, uint32_t l) { return l < (uint32_t)L.E ? L.qcap_s : L.qcap_a; }
 
 // one link's fields as uniform scalars
 struct LinkV {
@@ -301,7 +302,7 @@ __device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, const Ho
 // ---- link FIFO / transmitter (point-to-point-net-device.cc:273-336, 595-666)
 __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l, LinkV& k, uint32_t ring_idx,
                                                uint32_t x) {
-    const Layout& L = *S.L;
+    CLayout& L = *S.L;
     const bool sw = l < (uint32_t)L.E;
     int64_t tx = sw ? (ent_is_data(x) ? L.sw_txd : L.sw_txp) : S.acctx[l - (uint32_t)L.E];
     int64_t prop = sw ? L.sw_prop : 0;
@@ -318,7 +319,7 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
 // returns 1 if enqueued, 0 if dropped (a ring overflow fails the replica)
 template <int FS, int LS>
 __device__ __forceinline__ int link_send(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, uint32_t e) {
-    const Layout& L = *S.L;
+    CLayout& L = *S.L;
     LinkV k = link_get(R, l);
     uint32_t size = ent_size(L, e);
     bool ok = l < (uint32_t)L.E ? (k.qb + size <= L.qmax_bytes) : (k.n_queue + 1u <= L.acc_qmax_pkts);
@@ -344,7 +345,7 @@ __device__ __forceinline__ int link_send(const Sim& S, Regs<FS, LS>& R, Hot& H, 
 
 template <int FS, int LS>
 __device__ __forceinline__ void on_complete(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l) {   // :305-336
-    const Layout& L = *S.L;
+    CLayout& L = *S.L;
     LinkV k = link_get(R, l);
     k.busy = 0;
     if (k.n_queue) {
@@ -363,7 +364,7 @@ __device__ __forceinline__ void on_complete(const Sim& S, Regs<FS, LS>& R, Hot& 
 // ---- observation (data-packet-manager.cc:171-206)
 // send time in seconds of ping round k as the ping-back manager stores it:
 // (double)GetMilliSeconds() * 0.001 (ping-back-packet-manager.cc:98-116)
-__device__ __forceinline__ double ping_send_s(const Layout& L, int64_t k) {
+__device__ __forceinline__ double ping_send_s(CLayout& L, int64_t k) {
     uint64_t ms = (uint64_t)(((k + 1) * L.ping_period) / 1000000);
     return (double)ms * 0.001;
 }
@@ -440,7 +441,7 @@ __device__ __forceinline__ void patch_record(const Sim& S, const Hot& H, uint32_
 // Receive tail after the MacRx trace (point-to-point-net-device.cc:430-463).
 // arrived: a data packet at its destination (start = its start second).
 __device__ __forceinline__ void receive_counters(const Sim& S, const Hot& H, uint32_t x, bool arrived, uint32_t start) {
-    const Layout& L = *S.L;
+    CLayout& L = *S.L;
     if (S.lane == 0) {
         prisma_counters_t& c = *S.c;
         if (arrived) {
@@ -467,7 +468,7 @@ template <int FS, int LS>
 __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t x, uint32_t dst,
                                                uint32_t start, uint32_t uid, uint32_t v, uint32_t d, int action,
                                                bool fused, double reward, int32_t prev, uint32_t obs_reg) {
-    const Layout& L = *S.L;
+    CLayout& L = *S.L;
     int r0 = S.rowptr[v], deg = S.rowptr[v + 1] - r0;
     uint32_t status;
     if (action >= 0 && action < deg) {
@@ -504,7 +505,7 @@ __device__ __forceinline__ void finish_pending(const Sim& S, Regs<FS, LS>& R, Ho
 // ---- handlers (uniform) ------------------------------------------------------
 template <int FS, int LS>
 __device__ __forceinline__ void on_ping_round(const Sim& S, Regs<FS, LS>& R, Hot& H) {   // data-packet-manager.cc:350-413
-    const Layout& L = *S.L;
+    CLayout& L = *S.L;
     uint32_t k = H.ping_rounds;
     uint32_t first_rearm = 0;
     for (int u = 0; u < L.N; ++u) {
@@ -556,7 +557,7 @@ struct Decision {
 // returns 1 if a data decision needs an action
 template <int FS, int LS>
 __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, Decision& D, bool fused) {
-    const Layout& L = *S.L;
+    CLayout& L = *S.L;
     LinkV k = link_get(R, l);
     uint32_t cap = ring_cap(L, l);
     const uint32_t x = u_ld32(&S.ring[ring_off(L, l) + k.head]);
@@ -667,7 +668,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
 // ---------------------------------------------------------------------------
 template <int FS, int LS>
 __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t episode) {
-    const Layout& L = *S.L;
+    CLayout& L = *S.L;
     const int lane = S.lane;
     uint32_t dec = H.dec, hl = H.hops_launch;
     uint64_t ht = H.hops_total, et = H.events_total;
@@ -790,7 +791,7 @@ __device__ __forceinline__ void select_event(const Regs<FS, LS>& R, const Hot& H
 // ---------------------------------------------------------------------------
 // the [N][N] action table (table policy) sits in LDS after the state image
 __device__ __forceinline__ void stage_table(unsigned char* lds, const KParams& P, int lane) {
-    const Layout& L = *P.lay;
+    CLayout& L = *(CLayout*)P.lay;
     if (P.table) {
         uint8_t* dstp = lds + L.lds_state_bytes;
         const uint32_t nt = (uint32_t)(L.N * L.N);
@@ -800,7 +801,7 @@ __device__ __forceinline__ void stage_table(unsigned char* lds, const KParams& P
 
 template <int FS, int LS>
 __device__ __forceinline__ void stage_in(unsigned char* lds, const KParams& P, int r, int lane, Regs<FS, LS>& R) {
-    const Layout& L = *P.lay;
+    CLayout& L = *(CLayout*)P.lay;
     stage_table(lds, P, lane);
     const unsigned char* img = P.state + (size_t)r * L.state_bytes;
     const uint4* s4 = (const uint4*)img;
@@ -811,7 +812,7 @@ __device__ __forceinline__ void stage_in(unsigned char* lds, const KParams& P, i
 
 template <int FS, int LS>
 __device__ __forceinline__ void stage_out(unsigned char* lds, const KParams& P, int r, int lane, Regs<FS, LS>& R) {
-    const Layout& L = *P.lay;
+    CLayout& L = *(CLayout*)P.lay;
     unsigned char* img = P.state + (size_t)r * L.state_bytes;
     uint4* s4 = (uint4*)img;
     const uint4* d4 = (const uint4*)lds;
@@ -829,7 +830,7 @@ template <int FS, int LS>
 __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
-    const Layout& L = *P.lay;
+    CLayout& L = *(CLayout*)P.lay;
     Sim S;
     sim_bind(S, L, lds, P.topo, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r, lane);
     Regs<FS, LS> R;
@@ -842,11 +843,19 @@ __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     stage_out(lds, P, r, lane, R);
 }
 
+// waves per SIMD the register allocator must leave room for: 4 (<= 128
+// VGPRs) for small replicas so 4096 of them are resident on 256 CUs at
+// once, 2 (<= 256) up to 512 flows x 128 links
+template <int FS, int LS> struct StepOcc {
+    static constexpr int waves = (FS <= 2 && LS == 1) ? 4 : (LS <= 2 ? 2 : 1);
+};
+
 template <int FS, int LS>
-__global__ void __launch_bounds__(64) prisma_step_kernel_t(KParams P) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(StepOcc<FS, LS>::waves)))
+prisma_step_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
-    const Layout& L = *P.lay;
+    CLayout& L = *(CLayout*)P.lay;
     Regs<FS, LS> R;
     stage_in(lds, P, r, lane, R);
     __syncthreads();

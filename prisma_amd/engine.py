@@ -144,7 +144,14 @@ class PrismaEngine:
         sb, lb = C.c_uint32(), C.c_uint32()
         _check(L.prisma_state_bytes(self.h, C.byref(sb), C.byref(lb)))
         self.state_bytes, self.lds_bytes = int(sb.value), int(lb.value)
-        self.obs = torch.zeros((self.R, self.W), dtype=torch.int32, device=self.torch_device)
+        # register slots of the step-kernel instance the library picked (64 flows / links per slot)
+        fs, ls = 1, 1
+        while 64 * fs < topo.n_flows:
+            fs *= 2
+        while 64 * ls < topo.n_links + topo.n_nodes:
+            ls *= 2
+        self.kernel_name = f"prisma_step_kernel_t<{fs}, {ls}>"
+        self.obs =torch.zeros((self.R, self.W), dtype=torch.int32, device=self.torch_device)
         self.mask = torch.zeros(self.R, dtype=torch.uint8, device=self.torch_device)
         self.node = torch.zeros(self.R, dtype=torch.int32, device=self.torch_device)
 

@@ -14,7 +14,7 @@ os.makedirs(dst, exist_ok=True)
 
 
 def vals(path, counter):
-    rows = [r for r in csv.DictReader(open(path)) if r["Kernel_Name"] == "prisma_step_kernel" and r["Counter_Name"] == counter]
+    rows = [r for r in csv.DictReader(open(path)) if "prisma_step_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
     return [float(r["Counter_Value"]) for r in rows]
 
 
@@ -24,7 +24,8 @@ bench = json.loads(open(os.path.join(src, "bench.json")).read().strip().splitlin
 cfg = bench["config"]
 f_kb, w_kb = statistics.median(fetch[1:] or fetch), statistics.median(write[1:] or write)
 out = {
-    "kernel": "prisma_step_kernel", "replicas": cfg["replicas_per_gpu"], "hops": cfg["hops_per_step"],
+    "kernel": bench["roofline"]["kernel"], "kernel_source": bench["roofline"]["kernel_source"],
+    "topology": cfg["topology"], "replicas": cfg["replicas_per_gpu"], "hops": cfg["hops_per_step"],
     "fetch_size_kb_median": f_kb, "write_size_kb_median": w_kb,
     "read_bytes_per_launch": 2 * f_kb * 1024, "write_bytes_per_launch": w_kb * 1024,
     "bytes_per_launch": 2 * f_kb * 1024 + w_kb * 1024,
@@ -36,4 +37,8 @@ shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, "
 shutil.copy(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), os.path.join(dst, "pmc_fetch_size.csv"))
 shutil.copy(os.path.join(src, "pmc_write", "run_counter_collection.csv"), os.path.join(dst, "pmc_write_size.csv"))
 shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
+for sub in ("a", "b", "c"):                     # SQ instruction-mix / stall passes (scripts/pmc_sq.sh)
+    f = os.path.join(src, "sq", sub, "run_counter_collection.csv")
+    if os.path.exists(f):
+        shutil.copy(f, os.path.join(dst, f"pmc_sq_{sub}.csv"))
 print(json.dumps(out, indent=1))
