@@ -38,6 +38,13 @@ using namespace prisma;
 
 #define HIP_OK(x) ((x) == hipSuccess)
 
+// Diagnostic timing builds only (scripts/ablate.sh; results are NOT the
+// reference's): bit 0 skips the previous-record read (relay entries carry
+// dst/start), bit 1 skips the decision-record stores, bit 2 skips observe().
+#ifndef PRISMA_ABLATE
+#define PRISMA_ABLATE 0
+#endif
+
 // ---------------------------------------------------------------------------
 // kernel parameters
 // ---------------------------------------------------------------------------
@@ -399,6 +406,7 @@ template <int FS, int LS>
 __device__ __forceinline__ uint32_t observe(const Sim& S, const Regs<FS, LS>& R, const Hot& H, uint32_t v,
                                             uint32_t dst, double now_s) {
     uint32_t o = (S.lane == 0) ? dst : 0u;
+    if (PRISMA_ABLATE & 4) return o;
     int r0 = S.rowptr[v], r1 = S.rowptr[v + 1];
     for (int l = r0; l < r1; ++l) {
         uint32_t val = S.L->ping_as_obs ? ping_value(R, H, (uint32_t)l, now_s) : R.qb.get((uint32_t)l);
@@ -411,6 +419,7 @@ __device__ __forceinline__ uint32_t observe(const Sim& S, const Regs<FS, LS>& R,
 __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_t d, double reward, uint32_t uid,
                                              int32_t prev, uint32_t node, uint32_t dst, uint32_t start, int action,
                                              uint32_t status, uint32_t obs_reg) {
+    if (PRISMA_ABLATE & 2) return;
     const int lane = S.lane;
     uint64_t rb = __double_as_longlong(reward);
     uint32_t w7 = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
@@ -432,6 +441,7 @@ __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_
 }
 
 __device__ __forceinline__ void patch_record(const Sim& S, const Hot& H, uint32_t d, int action, uint32_t status) {
+    if (PRISMA_ABLATE & 2) return;
     if (S.lane == 0) {
         unsigned char* p = S.logrep + (size_t)(d & (S.L->log_cap - 1)) * S.L->rec_bytes;
         *(uint32_t*)(p + 28) = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
@@ -475,7 +485,8 @@ __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Ho
         uint32_t l = (uint32_t)(r0 + action);
         CNT(S, hops)++;
         CNT(S, hop_deg_sum) += (uint64_t)deg;
-        if (link_send(S, R, H, l, r_make(d))) {                   // lastHop = v, previous decision = d
+        const uint32_t fwd = (PRISMA_ABLATE & 1) ? (T_RELAY | (dst << 2) | (start << 10)) : r_make(d);
+        if (link_send(S, R, H, l, fwd)) {                         // lastHop = v, previous decision = d
             status = PRISMA_ST_ENQUEUED;
         } else {
             status = PRISMA_ST_DROPPED;              // :655-664 + forwarder.py:214-244
@@ -582,6 +593,8 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             start = s0 - ((s0 ^ f_parity(x)) & 1u);
             const uint32_t last = H.uid - 1u;
             uid = last - ((last - f_uid(x)) & kUidMask);
+        } else if (PRISMA_ABLATE & 1) {
+            dst = (x >> 2) & 255u; start = x >> 10; uid = 0; prev = (int32_t)d - 1;
         } else {
             // previous decision record (t_ns, uid, dst, start) from the HBM
             // log: the temp_obs entry of forwarder.py:153-159
@@ -756,6 +769,29 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return rdl(v, 63);
 }
 
+// One DPP step of an unsigned min, folded by the compiler into v_min_u32
+// with a DPP source: rows outside ROW_MASK see the identity (~0u).
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_umin(uint32_t v) {
+    uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, CTRL, ROW_MASK, 0xf, false);
+    return o < v ? o : v;
+}
+
+__device__ __forceinline__ uint32_t wave_umin_fast(uint32_t v) {
+    v = dpp_umin<0xB1, 0xF>(v);
+    v = dpp_umin<0x4E, 0xF>(v);
+    v = dpp_umin<0x141, 0xF>(v);
+    v = dpp_umin<0x140, 0xF>(v);
+    v = dpp_umin<0x142, 0xA>(v);
+    v = dpp_umin<0x143, 0xC>(v);
+    return rdl(v, 63);
+}
+
+// Next event = min (time, seq) over every source of the replica.  Each lane
+// first reduces the sources it owns (64-bit keys); the wave then reduces the
+// lane minima as 32-bit offsets from the clock (every pending event is at
+// most 2^32-2 ns ahead in practice; if none is, the exact 64-bit reduction
+// runs instead).
 template <int FS, int LS>
 __device__ __forceinline__ void select_event(const Regs<FS, LS>& R, const Hot& H, int lane, int64_t& bt, uint32_t& bc) {
     int64_t t = INT64_MAX;
@@ -773,16 +809,25 @@ __device__ __forceinline__ void select_event(const Regs<FS, LS>& R, const Hot& H
         if (key_less(tj, sj, t, s)) { t = tj; s = sj; c = (R.lk_kind.v[j] << 28) | (uint32_t)(lane + 64 * j); }
     }
     if (lane == 0 && key_less(H.ping_t, H.ping_seq, t, s)) { t = H.ping_t; s = H.ping_seq; c = K_PING << 28; }
-    const int64_t tmin = wave_min_i64(t);
-    uint64_t tied = __ballot(t == tmin);
+    const uint64_t dt = (uint64_t)(t - H.now);
+    const uint32_t key = (dt >> 32) ? 0xffffffffu : (uint32_t)dt;
+    const uint32_t kmin = wave_umin_fast(key);
+    bool tie;
+    if (kmin != 0xffffffffu) {
+        bt = H.now + (int64_t)kmin;
+        tie = (key == kmin);
+    } else {
+        bt = wave_min_i64(t);
+        tie = (t == bt);
+    }
+    const uint64_t tied = __ballot(tie);
     uint32_t win;
     if ((tied & (tied - 1)) == 0) {
         win = (uint32_t)__builtin_ctzll(tied);
     } else {                                                        // same-ns events: ns-3 uid order
-        uint32_t smin = wave_min_u32(t == tmin ? s : 0xffffffffu);
-        win = (uint32_t)__builtin_ctzll(__ballot(t == tmin && s == smin));
+        uint32_t smin = wave_umin_fast(tie ? s : 0xffffffffu);
+        win = (uint32_t)__builtin_ctzll(__ballot(tie && s == smin));
     }
-    bt = tmin;
     bc = rdl(c, win);
 }
 

@@ -56,11 +56,14 @@ EXPORTS = [
 _lib = None
 
 
-def load_library(path: str = LIB_PATH):
-    """Load libprisma_amd.so and declare its C-ABI (raises if absent)."""
+def load_library(path: str = None):
+    """Load libprisma_amd.so and declare its C-ABI (raises if absent).
+
+    PRISMA_LIB overrides the path (diagnostic builds, e.g. scripts/ablate.sh)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("PRISMA_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise PrismaError(f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     L = C.CDLL(path)
@@ -151,7 +154,7 @@ class PrismaEngine:
         while 64 * ls < topo.n_links + topo.n_nodes:
             ls *= 2
         self.kernel_name = f"prisma_step_kernel_t<{fs}, {ls}>"
-        self.obs =torch.zeros((self.R, self.W), dtype=torch.int32, device=self.torch_device)
+        self.obs = torch.zeros((self.R, self.W), dtype=torch.int32, device=self.torch_device)
         self.mask = torch.zeros(self.R, dtype=torch.uint8, device=self.torch_device)
         self.node = torch.zeros(self.R, dtype=torch.int32, device=self.torch_device)
 
