@@ -44,6 +44,15 @@ using namespace prisma;
 #ifndef PRISMA_ABLATE
 #define PRISMA_ABLATE 0
 #endif
+// Diagnostic timing build (-DPRISMA_TIMING=1, scripts/timing.py): s_memtime
+// cycle totals per loop phase, summed over waves into g_prisma_timing.
+#ifndef PRISMA_TIMING
+#define PRISMA_TIMING 0
+#endif
+#if PRISMA_TIMING
+__device__ unsigned long long g_prisma_timing[16];
+#define TM_NOW() ((uint64_t)__builtin_amdgcn_s_memtime())
+#endif
 
 // ---------------------------------------------------------------------------
 // kernel parameters
@@ -112,6 +121,84 @@ struct LA {
     }
 };
 
+// Per-episode counters updated in the event loop live in a register pair
+// (cv_lo, cv_hi): lane k holds counter slot k as 64 bits.  An update is a
+// full-wave add + select (no LDS read-modify-write to wait on); the slots are
+// moved from / to the prisma_counters_t image in LDS at launch entry / exit.
+enum CSlot : uint32_t {
+    C_EVENTS = 0, C_HOPS, C_DECISIONS, C_HOPDEG, C_REWARD, C_OV_INJ, C_OV_ARR, C_OV_LOST, C_BYTES_DATA,
+    C_BYTES_SIG, C_COST, C_E2E, C_COST_N, C_E2E_N, C_CTRL_DROP, C_NSLOTS
+};
+// byte offset and width (8: 64-bit) of each slot in prisma_counters_t
+__device__ __forceinline__ void cslot_field(uint32_t k, uint32_t& off, bool& wide) {
+    switch (k) {
+    case C_EVENTS: off = offsetof(prisma_counters_t, events); wide = true; break;
+    case C_HOPS: off = offsetof(prisma_counters_t, hops); wide = true; break;
+    case C_DECISIONS: off = offsetof(prisma_counters_t, decisions); wide = true; break;
+    case C_HOPDEG: off = offsetof(prisma_counters_t, hop_deg_sum); wide = true; break;
+    case C_REWARD: off = offsetof(prisma_counters_t, reward_sum); wide = true; break;
+    case C_OV_INJ: off = offsetof(prisma_counters_t, ov_injected); wide = false; break;
+    case C_OV_ARR: off = offsetof(prisma_counters_t, ov_arrived); wide = false; break;
+    case C_OV_LOST: off = offsetof(prisma_counters_t, ov_lost); wide = false; break;
+    case C_BYTES_DATA: off = offsetof(prisma_counters_t, bytes_data); wide = false; break;
+    case C_BYTES_SIG: off = offsetof(prisma_counters_t, bytes_signaling); wide = false; break;
+    case C_COST: off = offsetof(prisma_counters_t, cost_sum); wide = false; break;
+    case C_E2E: off = offsetof(prisma_counters_t, e2e_sum); wide = false; break;
+    case C_COST_N: off = offsetof(prisma_counters_t, cost_n); wide = false; break;
+    case C_E2E_N: off = offsetof(prisma_counters_t, e2e_n); wide = false; break;
+    default: off = offsetof(prisma_counters_t, ctrl_dropped); wide = false; break;
+    }
+}
+
+// lane id the compiler cannot hoist comparisons of out of the event loop
+// (15 hoisted lane masks would cost 30 SGPRs)
+__device__ __forceinline__ uint32_t fresh_lane() {
+    uint32_t l = threadIdx.x;
+    asm volatile("" : "+v"(l));
+    return l;
+}
+
+struct CntV {
+    uint32_t lo, hi;
+    template <uint32_t K> __device__ __forceinline__ void add_u64(uint64_t v) {
+        const uint64_t n = (((uint64_t)hi << 32) | lo) + v;
+        const bool me = fresh_lane() == K;
+        lo = me ? (uint32_t)n : lo;
+        hi = me ? (uint32_t)(n >> 32) : hi;
+    }
+    template <uint32_t K> __device__ __forceinline__ void add_u32(uint32_t v) {
+        lo = (fresh_lane() == K) ? lo + v : lo;
+    }
+    template <uint32_t K> __device__ __forceinline__ void add_f32(float v) {
+        lo = (fresh_lane() == K) ? __float_as_uint(__uint_as_float(lo) + v) : lo;
+    }
+    template <uint32_t K> __device__ __forceinline__ void add_f64(double v) {
+        const uint64_t n = __double_as_longlong(__longlong_as_double((long long)(((uint64_t)hi << 32) | lo)) + v);
+        const bool me = fresh_lane() == K;
+        lo = me ? (uint32_t)n : lo;
+        hi = me ? (uint32_t)(n >> 32) : hi;
+    }
+    __device__ __forceinline__ void load(const prisma_counters_t* c, uint32_t lane) {
+        lo = 0; hi = 0;
+        if (lane < C_NSLOTS) {
+            uint32_t off; bool wide;
+            cslot_field(lane, off, wide);
+            const uint32_t* w = (const uint32_t*)((const unsigned char*)c + off);
+            lo = w[0];
+            hi = wide ? w[1] : 0u;
+        }
+    }
+    __device__ __forceinline__ void store(prisma_counters_t* c, uint32_t lane) const {
+        if (lane < C_NSLOTS) {
+            uint32_t off; bool wide;
+            cslot_field(lane, off, wide);
+            uint32_t* w = (uint32_t*)((unsigned char*)c + off);
+            w[0] = lo;
+            if (wide) w[1] = hi;
+        }
+    }
+};
+
 // register-resident replica state (image order: the fields below, each a
 // [64*S] u32 array)
 template <int FS, int LS>
@@ -124,6 +211,7 @@ struct Regs {
     LA<LS> pav_lo, pav_hi;                       // ping window mean (double), refreshed per ping-back
     LA<LS> nd_lo, nd_hi, hd_lo, hd_hi;           // send time (s) of ping ack+1 and of the first hole
     static constexpr int NF = 4, NL = 20;
+    CntV cv;                                     // episode counters (not part of the register image)
 };
 
 template <int FS, int LS>
@@ -149,8 +237,6 @@ struct Hot {
     uint64_t hops_total, events_total;
 };
 
-// counters live in LDS and are updated by lane 0 only (keeps them out of SGPRs)
-#define CNT(S_, field_) if ((S_).lane == 0) (S_).c->field_
 
 // Read-only topology in HBM through the constant address space: every index
 // is wave-uniform, so these become s_load through the scalar cache.
@@ -229,7 +315,9 @@ __device__ inline void hot_load(const Sim& S, Hot& H) {
     H.events_total = (uint64_t)u_ld64((const int64_t*)&h.events_total);
 }
 
-__device__ inline void hot_store(Sim& S, const Hot& H) {
+template <int FS, int LS>
+__device__ inline void hot_store(Sim& S, const Regs<FS, LS>& R, const Hot& H) {
+    R.cv.store(S.c, (uint32_t)S.lane);
     if (S.lane == 0) {
         Hdr& h = *S.h;
         h.now = H.now; h.ping_t = H.ping_t; h.ping_seq = H.ping_seq; h.seq = H.seq; h.uid = H.uid;
@@ -380,39 +468,48 @@ __device__ __forceinline__ double ld_d(uint32_t lo, uint32_t hi) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-// 1000 * max(mean(window), min(now - oldest unacknowledged send, 2.6)) for
-// tunnel l.  Acknowledgements of one tunnel arrive in index order, so the
-// oldest pending entry is the first hole below the last ack, else the ping
-// after the last ack if it was sent.  The window mean and both candidate send
-// times are cached per link and refreshed on every ping-back.
-template <int FS, int LS>
-__device__ __forceinline__ uint32_t ping_value(const Regs<FS, LS>& R, const Hot& H, uint32_t l, double now_s) {
-    double avg = ld_d(R.pav_lo.get(l), R.pav_hi.get(l));
-    int32_t hole = (int32_t)R.pm_hole.get(l), acked = (int32_t)R.pm_ack.get(l);
-    float mt = 0.0f;
-    bool pend = hole >= 0 || (int64_t)acked + 1 < (int64_t)H.ping_rounds;
-    if (pend) {
-        double od = hole >= 0 ? ld_d(R.hd_lo.get(l), R.hd_hi.get(l)) : ld_d(R.nd_lo.get(l), R.nd_hi.get(l));
-        double a = now_s - od;
-        double b = 2.60;
-        mt = (float)((b < a) ? b : a);
-    }
-    double mx = (avg < (double)mt) ? (double)mt : avg;
+// 1000 * max(mean(window), min(now - oldest unacknowledged send, 2.6)) of a
+// tunnel (data-packet-manager.cc:171-206).  Acknowledgements of one tunnel
+// arrive in index order, so the oldest pending entry is the first hole below
+// the last ack, else the ping after the last ack if it was sent.  The window
+// mean and both candidate send times are cached per link and refreshed on
+// every ping-back.  Evaluated per lane for the links the lane owns.
+__device__ __forceinline__ uint32_t ping_value_lane(double avg, int32_t hole, int32_t acked, double hd, double nd,
+                                                    uint32_t rounds, double now_s) {
+    const bool pend = hole >= 0 || (int64_t)acked + 1 < (int64_t)rounds;
+    const double od = hole >= 0 ? hd : nd;
+    const double a = now_s - od;
+    const double b = 2.60;
+    const float mt = pend ? (float)((b < a) ? b : a) : 0.0f;
+    const double mx = (avg < (double)mt) ? (double)mt : avg;
     return (uint32_t)(1000 * mx);
 }
 
-// observation words in a per-lane register: lane i holds obs[i]
+// Observation of node v as a per-lane register (lane i holds obs[i], lane 0
+// left 0 for the destination): every lane evaluates the links it owns in
+// parallel, then lane i pulls link rowptr[v] + i - 1 with one permute per
+// register slot.
 template <int FS, int LS>
-__device__ __forceinline__ uint32_t observe(const Sim& S, const Regs<FS, LS>& R, const Hot& H, uint32_t v,
-                                            uint32_t dst, double now_s) {
-    uint32_t o = (S.lane == 0) ? dst : 0u;
-    if (PRISMA_ABLATE & 4) return o;
-    int r0 = S.rowptr[v], r1 = S.rowptr[v + 1];
-    for (int l = r0; l < r1; ++l) {
-        uint32_t val = S.L->ping_as_obs ? ping_value(R, H, (uint32_t)l, now_s) : R.qb.get((uint32_t)l);
-        o = wrl(o, val, (uint32_t)(1 + l - r0));
+__device__ __forceinline__ uint32_t observe_links(const Sim& S, const Regs<FS, LS>& R, const Hot& H, uint32_t v,
+                                                  double now_s) {
+    if (PRISMA_ABLATE & 4) return 0u;
+    const int r0 = S.rowptr[v], deg = S.rowptr[v + 1] - r0;
+    const int lane = S.lane;
+    const uint32_t src = (uint32_t)(r0 + lane - 1);
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < LS; ++j) {
+        uint32_t val;
+        if (S.L->ping_as_obs)
+            val = ping_value_lane(ld_d(R.pav_lo.v[j], R.pav_hi.v[j]), (int32_t)R.pm_hole.v[j], (int32_t)R.pm_ack.v[j],
+                                  ld_d(R.hd_lo.v[j], R.hd_hi.v[j]), ld_d(R.nd_lo.v[j], R.nd_hi.v[j]), H.ping_rounds,
+                                  now_s);
+        else
+            val = R.qb.v[j];
+        const uint32_t g = (uint32_t)__shfl((int)val, (int)(src & 63u));
+        if ((src >> 6) == (uint32_t)j) o = g;
     }
-    return o;
+    return (lane >= 1 && lane <= deg) ? o : 0u;
 }
 
 // one coalesced wave store of a decision record (lane i writes word i)
@@ -450,23 +547,24 @@ __device__ __forceinline__ void patch_record(const Sim& S, const Hot& H, uint32_
 
 // Receive tail after the MacRx trace (point-to-point-net-device.cc:430-463).
 // arrived: a data packet at its destination (start = its start second).
-__device__ __forceinline__ void receive_counters(const Sim& S, const Hot& H, uint32_t x, bool arrived, uint32_t start) {
+template <int FS, int LS>
+__device__ __forceinline__ void receive_counters(const Sim& S, Regs<FS, LS>& R, const Hot& H, uint32_t x, bool arrived,
+                                                 uint32_t start) {
     CLayout& L = *S.L;
-    if (S.lane == 0) {
-        prisma_counters_t& c = *S.c;
-        if (arrived) {
-            // valable, nextHop == finalDest on identity overlays
-            c.ov_arrived++;
-            float cost = (float)(ns_to_sec(H.now) - (double)start);
-            c.cost_sum += cost; c.cost_n++;
-            c.e2e_sum += cost; c.e2e_n++;
-        }
-        // pings are always addressed to the node that receives them
-        if (!ent_is_data(x)) c.bytes_signaling += (int32_t)(L.ping_size - 2);
-        if (ent_type(x) == T_FRESH) {
-            c.ov_injected++;
-            c.bytes_data += (int32_t)(L.data_size - 2);
-        }
+    if (arrived) {
+        // valable, nextHop == finalDest on identity overlays
+        R.cv.template add_u32<C_OV_ARR>(1u);
+        const float cost = (float)(ns_to_sec(H.now) - (double)start);
+        R.cv.template add_f32<C_COST>(cost);
+        R.cv.template add_u32<C_COST_N>(1u);
+        R.cv.template add_f32<C_E2E>(cost);
+        R.cv.template add_u32<C_E2E_N>(1u);
+    }
+    // pings are always addressed to the node that receives them
+    if (!ent_is_data(x)) R.cv.template add_u32<C_BYTES_SIG>(L.ping_size - 2u);
+    if (ent_type(x) == T_FRESH) {
+        R.cv.template add_u32<C_OV_INJ>(1u);
+        R.cv.template add_u32<C_BYTES_DATA>(L.data_size - 2u);
     }
 }
 
@@ -483,26 +581,24 @@ __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Ho
     uint32_t status;
     if (action >= 0 && action < deg) {
         uint32_t l = (uint32_t)(r0 + action);
-        CNT(S, hops)++;
-        CNT(S, hop_deg_sum) += (uint64_t)deg;
+        R.cv.template add_u64<C_HOPS>(1u);
+        R.cv.template add_u64<C_HOPDEG>((uint64_t)deg);
         const uint32_t fwd = (PRISMA_ABLATE & 1) ? (T_RELAY | (dst << 2) | (start << 10)) : r_make(d);
         if (link_send(S, R, H, l, fwd)) {                         // lastHop = v, previous decision = d
             status = PRISMA_ST_ENQUEUED;
         } else {
             status = PRISMA_ST_DROPPED;              // :655-664 + forwarder.py:214-244
-            if (S.lane == 0) {
-                S.c->ov_lost++;
-                S.c->cost_sum += L.loss_penalty_f;
-                S.c->cost_n++;
-                S.c->reward_sum += L.loss_penalty;
-            }
+            R.cv.template add_u32<C_OV_LOST>(1u);
+            R.cv.template add_f32<C_COST>(L.loss_penalty_f);
+            R.cv.template add_u32<C_COST_N>(1u);
+            R.cv.template add_f64<C_REWARD>(L.loss_penalty);
         }
     } else {
         status = PRISMA_ST_DISCARDED;
     }
     if (fused) write_record(S, H, d, reward, uid, prev, v, dst, start, action, status, obs_reg);
     else patch_record(S, H, d, action, status);
-    receive_counters(S, H, x, false, 0u);
+    receive_counters(S, R, H, x, false, 0u);
 }
 
 template <int FS, int LS>
@@ -522,14 +618,14 @@ __device__ __forceinline__ void on_ping_round(const Sim& S, Regs<FS, LS>& R, Hot
     for (int u = 0; u < L.N; ++u) {
         int r0 = S.rowptr[u], r1 = S.rowptr[u + 1];
         for (int l = r0; l < r1; ++l) {
-            if (!link_send(S, R, H, (uint32_t)l, p_make(T_PFWD, (uint32_t)(l - r0), k))) CNT(S, ctrl_dropped)++;
+            if (!link_send(S, R, H, (uint32_t)l, p_make(T_PFWD, (uint32_t)(l - r0), k))) R.cv.template add_u32<C_CTRL_DROP>(1u);
         }
         uint32_t s = H.seq++;                                    // re-arm of node u
         if (u == 0) first_rearm = s;
     }
     H.ping_rounds = k + 1;
     // one ns-3 event per node timer (the round is N consecutive events)
-    CNT(S, events) += (uint64_t)(L.N - 1);
+    R.cv.template add_u64<C_EVENTS>((uint64_t)(L.N - 1));
     H.events_total += (uint64_t)(L.N - 1);
     H.ping_t = H.now + L.ping_period;
     H.ping_seq = first_rearm;
@@ -572,14 +668,28 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     LinkV k = link_get(R, l);
     uint32_t cap = ring_cap(L, l);
     const uint32_t x = u_ld32(&S.ring[ring_off(L, l) + k.head]);
+    const uint32_t type = ent_type(x);
+    // a forwarded packet's previous decision record (t_ns, uid, dst, start)
+    // from the HBM log -- the temp_obs entry of forwarder.py:153-159.  The
+    // load is issued here and consumed after the link update and the
+    // observation, which do not depend on it.
+    const uint32_t d = H.dec;
+    const uint32_t dist = (d - r_dec(x)) & kRelayMask;
+    uint4 ph = make_uint4(0, 0, 0, 0);
+    uint32_t w6 = 0;
+    if (type == T_RELAY && !(PRISMA_ABLATE & 1)) {
+        const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap - 1)) * L.rec_bytes;
+        ph = *(const uint4*)pr;
+        w6 = *(const uint32_t*)(pr + 24);
+    }
     k.head = (k.head + 1 == cap) ? 0 : k.head + 1;
     k.n_wire--;
     link_put(S, R, H, l, k);
     const uint32_t v = (uint32_t)S.ldst[l];
-    const uint32_t type = ent_type(x);
     if (ent_is_data(x)) {
         // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
-        const uint32_t d = H.dec++;
+        H.dec = d + 1u;
+        const uint32_t obs_links = observe_links(S, R, H, v, ns_to_sec(H.now));
         double reward = 0.0;
         int32_t prev = -1;
         uint32_t dst, start, uid;
@@ -596,26 +706,21 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
         } else if (PRISMA_ABLATE & 1) {
             dst = (x >> 2) & 255u; start = x >> 10; uid = 0; prev = (int32_t)d - 1;
         } else {
-            // previous decision record (t_ns, uid, dst, start) from the HBM
-            // log: the temp_obs entry of forwarder.py:153-159
-            const uint32_t dist = (d - r_dec(x)) & kRelayMask;
             prev = (int32_t)(d - dist);
             if (dist >= L.log_cap) fail(H, PRISMA_EBIT_LOGWRAP);
-            const unsigned char* pr = S.logrep + (size_t)((uint32_t)prev & (L.log_cap - 1)) * L.rec_bytes;
-            const uint4 ph = *(const uint4*)pr;
-            const uint32_t w6 = rfl(*(const uint32_t*)(pr + 24));
             const int64_t t_prev = mk64(rfl(ph.x), rfl(ph.y));
             uid = rfl(ph.z);
-            dst = (w6 >> 8) & 255u;
-            start = w6 >> 16;
+            const uint32_t w = rfl(w6);
+            dst = (w >> 8) & 255u;
+            start = w >> 16;
             reward = (double)py_micros(H.now) / 1e6 - (double)py_micros(t_prev) / 1e6;   // forwarder.py:360
-            CNT(S, reward_sum) += reward;
+            R.cv.template add_f64<C_REWARD>(reward);
         }
-        uint32_t o = observe(S, R, H, v, dst, ns_to_sec(H.now));
-        CNT(S, decisions)++;
+        const uint32_t o = (S.lane == 0) ? dst : obs_links;
+        R.cv.template add_u64<C_DECISIONS>(1u);
         if (dst == v) {                                             // getGameOver
             write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_DESTINATION, o);
-            receive_counters(S, H, x, true, start);
+            receive_counters(S, R, H, x, true, start);
             return 0;
         }
         if (!fused) write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_PENDING, o);
@@ -627,7 +732,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     if (type == T_PFWD) {                                           // ping-forward-packet-manager.cc:94-156
         float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
         if (S.lane == 0) S.pbd[l * L.PBK + (rnd & (L.PBK - 1))] = delay;
-        if (!link_send(S, R, H, (uint32_t)S.lrev[l], p_make(T_PBACK, tun, rnd))) CNT(S, ctrl_dropped)++;
+        if (!link_send(S, R, H, (uint32_t)S.lrev[l], p_make(T_PBACK, tun, rnd))) R.cv.template add_u32<C_CTRL_DROP>(1u);
     } else {                                                        // ping-back-packet-manager.cc:120-144
         const uint32_t lt = (uint32_t)S.rowptr[v] + tun;
         const float delay = __uint_as_float(u_ld32((const uint32_t*)S.pbd + lt * L.PBK + (rnd & (L.PBK - 1))));
@@ -672,7 +777,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
         R.pav_lo.set(lt, (uint32_t)avg);
         R.pav_hi.set(lt, (uint32_t)(avg >> 32));
     }
-    receive_counters(S, H, x, false, 0u);
+    receive_counters(S, R, H, x, false, 0u);
     return 0;
 }
 
@@ -688,6 +793,8 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
     __syncthreads();
     uint4* st4 = (uint4*)S.base;
     for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
+    R.cv.lo = 0;
+    R.cv.hi = 0;
 #pragma unroll
     for (int j = 0; j < FS; ++j) {
         uint32_t f = (uint32_t)lane + 64u * j;
@@ -882,7 +989,7 @@ __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     Hot H;
     memset(&H, 0, sizeof(H));
     init_replica(S, R, H, P.episode);
-    hot_store(S, H);
+    hot_store(S, R, H);
     __syncthreads();
     publish_counters(S, P, r, lane);
     stage_out(lds, P, r, lane, R);
@@ -911,6 +1018,7 @@ prisma_step_kernel_t(KParams P) {
     const uint32_t NN = (uint32_t)L.N;
     Hot H;
     hot_load(S, H);
+    R.cv.load(S.c, (uint32_t)lane);
 
     H.stop = 0;
     H.hops_launch = 0;
@@ -929,9 +1037,20 @@ prisma_step_kernel_t(KParams P) {
     if (H.over || (table_mode && H.hops_launch >= max_hops)) H.stop = 1;
 
     uint32_t resets = 0;
+#if PRISMA_TIMING
+    uint64_t tm_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t tm_cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t tm_a = 0, tm_b = 0;
+#define TM_MARK(i) do { tm_b = TM_NOW(); tm_acc[i] += tm_b - tm_a; tm_cnt[i]++; tm_a = tm_b; } while (0)
+#else
+#define TM_MARK(i) do { } while (0)
+#endif
     while (!H.stop) {
         int64_t bt;
         uint32_t bc;
+#if PRISMA_TIMING
+        tm_a = TM_NOW();
+#endif
         select_event(R, H, lane, bt, bc);
         if (bt >= L.t_end) {                           // Simulator::Stop(simTime) (sim.cc:703)
             if (L.auto_reset && resets < 64u) {        // bounded: an empty scenario cannot spin forever
@@ -944,12 +1063,15 @@ prisma_step_kernel_t(KParams P) {
             break;
         }
         H.now = bt;
-        CNT(S, events)++;
+        R.cv.template add_u64<C_EVENTS>(1u);
         H.events_total++;
         const uint32_t kind = bc >> 28, id = bc & 0x0fffffffu;
+        TM_MARK(0);
         if (kind == K_ARRIVE) {
             Decision D;
-            if (on_arrive(S, R, H, id, D, table_mode)) {
+            const int need = on_arrive(S, R, H, id, D, table_mode);
+            TM_MARK(1);
+            if (need) {
                 if (table_mode) {
                     int a = (int)S.table[D.v * NN + D.dst];
                     apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, (int)rfl((uint32_t)a), true,
@@ -957,6 +1079,7 @@ prisma_step_kernel_t(KParams P) {
                     H.hops_launch++;
                     H.hops_total++;
                     if (H.hops_launch >= max_hops) H.stop = 1;
+                    TM_MARK(2);
                 } else {
                     if (lane == 0) {
                         Hdr& h = *S.h;
@@ -970,15 +1093,26 @@ prisma_step_kernel_t(KParams P) {
             }
         } else if (kind == K_COMPLETE) {
             on_complete(S, R, H, id);
+            TM_MARK(3);
         } else if (kind == K_FLOW) {
             on_flow(S, R, H, id);
+            TM_MARK(4);
         } else {
             on_ping_round(S, R, H);
+            TM_MARK(5);
         }
         if (H.error) { H.over = 1; H.stop = 1; }
     }
+#if PRISMA_TIMING
+    if (lane == 0) {
+        for (int i = 0; i < 8; ++i) {
+            atomicAdd(&g_prisma_timing[i], (unsigned long long)tm_acc[i]);
+            atomicAdd(&g_prisma_timing[8 + i], (unsigned long long)tm_cnt[i]);
+        }
+    }
+#endif
 
-    hot_store(S, H);
+    hot_store(S, R, H);
     __syncthreads();
     const bool pending = H.pend && !H.over;
     if (P.mask_out && lane == 0) P.mask_out[r] = pending ? 1 : 0;
@@ -1041,6 +1175,16 @@ static thread_local std::string g_err;
 static int set_err(int code, const std::string& msg) { g_err = msg; return code; }
 
 extern "C" int prisma_abi_version(void) { return PRISMA_ABI_VERSION; }
+
+#if PRISMA_TIMING
+// diagnostic build only: read and clear the per-phase cycle totals
+extern "C" int prisma_debug_timing(unsigned long long* out16) {
+    if (!HIP_OK(hipDeviceSynchronize()) ||
+        !HIP_OK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prisma_timing), 16 * sizeof(unsigned long long)))) return -1;
+    unsigned long long z[16] = {0};
+    return HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_timing), z, sizeof(z))) ? 0 : -1;
+}
+#endif
 extern "C" const char* prisma_last_error(void) { return g_err.c_str(); }
 
 static uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
