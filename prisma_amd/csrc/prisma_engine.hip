@@ -204,8 +204,12 @@ struct CntV {
 template <int FS, int LS>
 struct Regs {
     LA<FS> fk_lo, fk_hi, fk_seq, f_draw;         // flow next event (time, seq) + draw index
-    LA<LS> lk_lo, lk_hi, lk_seq, lk_kind;        // link next event key: kind 0 none / K_COMPLETE / K_ARRIVE
-    LA<LS> cp_lo, cp_hi, cp_seq;                 // tx completion event (valid while busy)
+    // link times are kept as their low 32 bits: every pending link event is
+    // less than 2^31 ns ahead of the clock (checked on the host), so
+    // t = now + (uint32)(t_lo - lo32(now))
+    LA<LS> lk_t, lk_seq, lk_kind;                // link next event key: kind 0 none / K_COMPLETE / K_ARRIVE
+    LA<LS> cp_t, cp_seq;                         // tx completion event (valid while busy)
+    LA<LS> wh_t, wh_seq;                         // arrival event of the wire head (valid while n_wire > 0)
     LA<LS> p0, p1, p2, qb;                       // head|txp<<16, tail|n_wire<<16, n_queue|busy<<16, queued bytes
     LA<LS> pm_ack, pm_hole, pm_win;              // ping: last ack, first hole, win_n|win_head<<16
     LA<LS> pav_lo, pav_hi;                       // ping window mean (double), refreshed per ping-back
@@ -221,7 +225,7 @@ __device__ __forceinline__ void regs_io(Regs<FS, LS>& R, uint32_t* img, int lane
 #define RIO_F(fld, a) if (store) R.fld.store(fb + (a) * 64 * FS, lane); else R.fld.load(fb + (a) * 64 * FS, lane);
 #define RIO_L(fld, a) if (store) R.fld.store(lb + (a) * 64 * LS, lane); else R.fld.load(lb + (a) * 64 * LS, lane);
     RIO_F(fk_lo, 0) RIO_F(fk_hi, 1) RIO_F(fk_seq, 2) RIO_F(f_draw, 3)
-    RIO_L(lk_lo, 0) RIO_L(lk_hi, 1) RIO_L(lk_seq, 2) RIO_L(lk_kind, 3) RIO_L(cp_lo, 4) RIO_L(cp_hi, 5)
+    RIO_L(lk_t, 0) RIO_L(wh_t, 1) RIO_L(lk_seq, 2) RIO_L(lk_kind, 3) RIO_L(cp_t, 4) RIO_L(wh_seq, 5)
     RIO_L(cp_seq, 6) RIO_L(p0, 7) RIO_L(p1, 8) RIO_L(p2, 9) RIO_L(qb, 10) RIO_L(pm_ack, 11)
     RIO_L(pm_hole, 12) RIO_L(pm_win, 13) RIO_L(pav_lo, 14) RIO_L(pav_hi, 15) RIO_L(nd_lo, 16)
     RIO_L(nd_hi, 17) RIO_L(hd_lo, 18) RIO_L(hd_hi, 19)
@@ -352,8 +356,8 @@ __device__ __forceinline__ uint32_t ring_cap(CLayout& L, uint32_t l) { return l 
 // one link's fields as uniform scalars
 struct LinkV {
     uint32_t head, txp, tail, n_wire, n_queue, busy, qb;
-    int64_t cp_t;
-    uint32_t cp_seq;
+    uint32_t cp_t, cp_seq;       // completion time (low 32 bits), seq
+    uint32_t wh_t, wh_seq;       // wire-head arrival time (low 32 bits), seq
 };
 
 template <int FS, int LS>
@@ -364,32 +368,33 @@ __device__ __forceinline__ LinkV link_get(const Regs<FS, LS>& R, uint32_t l) {
     k.tail = b & 0xffffu; k.n_wire = b >> 16;
     k.n_queue = c & 0xffffu; k.busy = c >> 16;
     k.qb = R.qb.get(l);
-    k.cp_t = mk64(R.cp_lo.get(l), R.cp_hi.get(l));
+    k.cp_t = R.cp_t.get(l);
     k.cp_seq = R.cp_seq.get(l);
+    k.wh_t = R.wh_t.get(l);
+    k.wh_seq = R.wh_seq.get(l);
     return k;
 }
 
-// write back a link's fields and recompute its candidate key
+// write back a link's fields and recompute its candidate key (registers only:
+// the wire head's key is cached in wh_t / wh_seq)
 template <int FS, int LS>
 __device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, const Hot& H, uint32_t l, const LinkV& k) {
     R.p0.set(l, k.head | (k.txp << 16));
     R.p1.set(l, k.tail | (k.n_wire << 16));
     R.p2.set(l, k.n_queue | (k.busy << 16));
     R.qb.set(l, k.qb);
-    R.cp_lo.set(l, lo32(k.cp_t));
-    R.cp_hi.set(l, hi32(k.cp_t));
+    R.cp_t.set(l, k.cp_t);
     R.cp_seq.set(l, k.cp_seq);
-    int64_t t = INT64_MAX;
-    uint32_t s = 0xffffffffu, kind = 0;
+    R.wh_t.set(l, k.wh_t);
+    R.wh_seq.set(l, k.wh_seq);
+    const uint32_t n0 = lo32(H.now);
+    uint32_t t = 0, s = 0xffffffffu, kind = 0;
     if (k.busy) { t = k.cp_t; s = k.cp_seq; kind = K_COMPLETE; }
     if (k.n_wire) {
-        uint32_t w = l * (uint32_t)S.L->WCAP + (k.head & (uint32_t)(S.L->WCAP - 1));
-        int64_t wt = H.now + (int64_t)(uint32_t)(u_ld32(S.wt + w) - lo32(H.now));
-        uint32_t ws = u_ld32(S.wseq + w);
-        if (key_less(wt, ws, t, s)) { t = wt; s = ws; kind = K_ARRIVE; }
+        const uint32_t rw = k.wh_t - n0, rt = t - n0;
+        if (kind == 0 || rw < rt || (rw == rt && k.wh_seq < s)) { t = k.wh_t; s = k.wh_seq; kind = K_ARRIVE; }
     }
-    R.lk_lo.set(l, lo32(t));
-    R.lk_hi.set(l, hi32(t));
+    R.lk_t.set(l, t);
     R.lk_seq.set(l, s);
     R.lk_kind.set(l, kind);
 }
@@ -402,12 +407,13 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
     int64_t tx = sw ? (ent_is_data(x) ? L.sw_txd : L.sw_txp) : S.acctx[l - (uint32_t)L.E];
     int64_t prop = sw ? L.sw_prop : 0;
     k.busy = 1;
-    k.cp_t = H.now + tx;
+    k.cp_t = lo32(H.now + tx);
     k.cp_seq = H.seq++;                                        // TransmitComplete
     uint32_t w = l * (uint32_t)L.WCAP + (ring_idx & (uint32_t)(L.WCAP - 1));
-    int64_t at = H.now + tx + prop;
-    uint32_t as = H.seq++;                                     // channel Receive
-    if (S.lane == 0) { S.wt[w] = lo32(at); S.wseq[w] = as; }
+    const uint32_t at = lo32(H.now + tx + prop);
+    const uint32_t as = H.seq++;                               // channel Receive
+    if (S.lane == 0) { S.wt[w] = at; S.wseq[w] = as; }
+    if (k.n_wire == 1) { k.wh_t = at; k.wh_seq = as; }        // the wire was empty: new head
     if (k.n_wire > (uint32_t)L.WCAP) fail(H, PRISMA_EBIT_WIRE);
 }
 
@@ -657,6 +663,21 @@ __device__ __forceinline__ void on_flow(const Sim& S, Regs<FS, LS>& R, Hot& H, u
     flow_next(S, R, H, f, draw);                                    // StartSending / ScheduleNextTx
 }
 
+// the head packet leaves the wire of link l (arrival at the far end)
+template <int FS, int LS>
+__device__ __forceinline__ void wire_pop(const Sim& S, Regs<FS, LS>& R, const Hot& H, uint32_t l, LinkV& k) {
+    CLayout& L = *S.L;
+    const uint32_t cap = ring_cap(L, l);
+    k.head = (k.head + 1 == cap) ? 0 : k.head + 1;
+    k.n_wire--;
+    if (k.n_wire) {                                                 // next packet on the wire
+        const uint32_t w = l * (uint32_t)L.WCAP + (k.head & (uint32_t)(L.WCAP - 1));
+        k.wh_t = u_ld32(S.wt + w);
+        k.wh_seq = u_ld32(S.wseq + w);
+    }
+    link_put(S, R, H, l, k);
+}
+
 struct Decision {
     uint32_t x, dst, start, uid, v, d; double reward; int32_t prev; uint32_t obs;
 };
@@ -666,30 +687,29 @@ template <int FS, int LS>
 __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, Decision& D, bool fused) {
     CLayout& L = *S.L;
     LinkV k = link_get(R, l);
-    uint32_t cap = ring_cap(L, l);
     const uint32_t x = u_ld32(&S.ring[ring_off(L, l) + k.head]);
     const uint32_t type = ent_type(x);
-    // a forwarded packet's previous decision record (t_ns, uid, dst, start)
-    // from the HBM log -- the temp_obs entry of forwarder.py:153-159.  The
-    // load is issued here and consumed after the link update and the
-    // observation, which do not depend on it.
-    const uint32_t d = H.dec;
-    const uint32_t dist = (d - r_dec(x)) & kRelayMask;
-    uint4 ph = make_uint4(0, 0, 0, 0);
-    uint32_t w6 = 0;
-    if (type == T_RELAY && !(PRISMA_ABLATE & 1)) {
-        const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap - 1)) * L.rec_bytes;
-        ph = *(const uint4*)pr;
-        w6 = *(const uint32_t*)(pr + 24);
-    }
-    k.head = (k.head + 1 == cap) ? 0 : k.head + 1;
-    k.n_wire--;
-    link_put(S, R, H, l, k);
     const uint32_t v = (uint32_t)S.ldst[l];
     if (ent_is_data(x)) {
         // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
+        // A forwarded packet's previous decision record (t_ns, uid, dst,
+        // start) comes from the HBM log -- the temp_obs entry of
+        // forwarder.py:153-159.  The load is issued first and consumed after
+        // the link update and the observation, which do not depend on it
+        // (and only on this path, so no load is ever left in flight across
+        // loop iterations).
+        // (A fresh packet loads and ignores some record of its own log: the
+        // load and its consumption are unconditional on this path.)
+        const uint32_t d = H.dec;
+        const uint32_t dist = (d - r_dec(x)) & kRelayMask;
+        const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap - 1)) * L.rec_bytes;
+        const uint4 ph = *(const uint4*)pr;
+        const uint32_t w6 = *(const uint32_t*)(pr + 24);
+        wire_pop(S, R, H, l, k);
         H.dec = d + 1u;
         const uint32_t obs_links = observe_links(S, R, H, v, ns_to_sec(H.now));
+        const int64_t t_prev = mk64(rfl(ph.x), rfl(ph.y));
+        const uint32_t uid_prev = rfl(ph.z), w_prev = rfl(w6);
         double reward = 0.0;
         int32_t prev = -1;
         uint32_t dst, start, uid;
@@ -708,11 +728,9 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
         } else {
             prev = (int32_t)(d - dist);
             if (dist >= L.log_cap) fail(H, PRISMA_EBIT_LOGWRAP);
-            const int64_t t_prev = mk64(rfl(ph.x), rfl(ph.y));
-            uid = rfl(ph.z);
-            const uint32_t w = rfl(w6);
-            dst = (w >> 8) & 255u;
-            start = w >> 16;
+            uid = uid_prev;
+            dst = (w_prev >> 8) & 255u;
+            start = w_prev >> 16;
             reward = (double)py_micros(H.now) / 1e6 - (double)py_micros(t_prev) / 1e6;   // forwarder.py:360
             R.cv.template add_f64<C_REWARD>(reward);
         }
@@ -728,6 +746,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
         D.obs = o;
         return 1;
     }
+    wire_pop(S, R, H, l, k);
     const uint32_t tun = p_tunnel(x), rnd = p_round(x);
     if (type == T_PFWD) {                                           // ping-forward-packet-manager.cc:94-156
         float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
@@ -812,8 +831,8 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
     }
 #pragma unroll
     for (int j = 0; j < LS; ++j) {
-        R.lk_lo.v[j] = lo32(INT64_MAX); R.lk_hi.v[j] = hi32(INT64_MAX); R.lk_seq.v[j] = 0xffffffffu;
-        R.lk_kind.v[j] = 0; R.cp_lo.v[j] = 0; R.cp_hi.v[j] = 0; R.cp_seq.v[j] = 0;
+        R.lk_t.v[j] = 0; R.lk_seq.v[j] = 0xffffffffu; R.lk_kind.v[j] = 0;
+        R.cp_t.v[j] = 0; R.cp_seq.v[j] = 0; R.wh_t.v[j] = 0; R.wh_seq.v[j] = 0;
         R.p0.v[j] = 0; R.p1.v[j] = 0; R.p2.v[j] = 0; R.qb.v[j] = 0;
         R.pm_ack.v[j] = 0xffffffffu; R.pm_hole.v[j] = 0xffffffffu; R.pm_win.v[j] = 0;
         R.pav_lo.v[j] = 0; R.pav_hi.v[j] = 0;
@@ -833,9 +852,7 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
 }
 
 // ---------------------------------------------------------------------------
-// wave-wide event selection: per-lane min over owned register keys, a DPP
-// reduction of the 64-bit time to lane 63, and a second reduction of seq over
-// the tied lanes only when two sources share the nanosecond.
+// wave-wide reductions to lane 63 (DPP row/bank steps)
 // ---------------------------------------------------------------------------
 template <int CTRL, int ROW_MASK>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
@@ -850,12 +867,6 @@ __device__ __forceinline__ int64_t dpp_min_i64(int64_t v) {
     return o < v ? o : v;
 }
 
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint32_t dpp_min_u32(uint32_t v) {
-    uint32_t o = dpp_u32<CTRL, ROW_MASK>(v);
-    return o < v ? o : v;
-}
-
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
     v = dpp_min_i64<0xB1, 0xF>(v);      // quad_perm [1,0,3,2]
     v = dpp_min_i64<0x4E, 0xF>(v);      // quad_perm [2,3,0,1]
@@ -864,16 +875,6 @@ __device__ __forceinline__ int64_t wave_min_i64(int64_t v) {
     v = dpp_min_i64<0x142, 0xA>(v);     // row_bcast:15
     v = dpp_min_i64<0x143, 0xC>(v);     // row_bcast:31
     return mk64(rdl(lo32(v), 63), rdl(hi32(v), 63));
-}
-
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-    v = dpp_min_u32<0xB1, 0xF>(v);
-    v = dpp_min_u32<0x4E, 0xF>(v);
-    v = dpp_min_u32<0x141, 0xF>(v);
-    v = dpp_min_u32<0x140, 0xF>(v);
-    v = dpp_min_u32<0x142, 0xA>(v);
-    v = dpp_min_u32<0x143, 0xC>(v);
-    return rdl(v, 63);
 }
 
 // One DPP step of an unsigned min, folded by the compiler into v_min_u32
@@ -894,48 +895,79 @@ __device__ __forceinline__ uint32_t wave_umin_fast(uint32_t v) {
     return rdl(v, 63);
 }
 
-// Next event = min (time, seq) over every source of the replica.  Each lane
-// first reduces the sources it owns (64-bit keys); the wave then reduces the
-// lane minima as 32-bit offsets from the clock (every pending event is at
-// most 2^32-2 ns ahead in practice; if none is, the exact 64-bit reduction
-// runs instead).
+// Next event = min (time, seq) over every source of the replica, as 32-bit
+// offsets from the clock: each lane reduces the sources it owns
+// lexicographically on (offset, seq), the wave reduces the lane minima with
+// fused DPP min steps.  Link events are always < 2^31 ns ahead; a flow or the
+// ping timer further than 2^32-2 ns ahead saturates, and if every source
+// saturates the exact 64-bit reduction over flows and ping runs instead.
+__device__ __forceinline__ void key_take(uint32_t k, uint32_t s, uint32_t c, uint32_t& bk, uint32_t& bs,
+                                         uint32_t& bc) {
+    if (k < bk || (k == bk && s < bs)) { bk = k; bs = s; bc = c; }
+}
+
+__device__ __forceinline__ uint32_t sat_offset(int64_t t, int64_t now) {
+    const uint64_t dt = (uint64_t)(t - now);
+    return (dt >> 32) ? 0xffffffffu : (uint32_t)dt;
+}
+
 template <int FS, int LS>
 __device__ __forceinline__ void select_event(const Regs<FS, LS>& R, const Hot& H, int lane, int64_t& bt, uint32_t& bc) {
-    int64_t t = INT64_MAX;
+    // flows and the ping timer: exact 64-bit per-lane minimum, then one offset
+    int64_t ft = INT64_MAX;
     uint32_t s = 0xffffffffu, c = 0xffffffffu;
+#pragma unroll
+    for (int j = 0; j < FS; ++j) {
+        const int64_t tj = mk64(R.fk_lo.v[j], R.fk_hi.v[j]);
+        const uint32_t sj = R.fk_seq.v[j];
+        if (key_less(tj, sj, ft, s)) { ft = tj; s = sj; c = (K_FLOW << 28) | (uint32_t)(lane + 64 * j); }
+    }
+    if (lane == 0 && key_less(H.ping_t, H.ping_seq, ft, s)) { ft = H.ping_t; s = H.ping_seq; c = K_PING << 28; }
+    uint32_t k = sat_offset(ft, H.now);
+    // links: 32-bit offsets
+    const uint32_t n0 = lo32(H.now);
+#pragma unroll
+    for (int j = 0; j < LS; ++j) {
+        const uint32_t kind = R.lk_kind.v[j];
+        const uint32_t kj = kind ? R.lk_t.v[j] - n0 : 0xffffffffu;
+        key_take(kj, R.lk_seq.v[j], (kind << 28) | (uint32_t)(lane + 64 * j), k, s, c);
+    }
+    const uint32_t kmin = wave_umin_fast(k);
+    if (kmin != 0xffffffffu) {
+        bt = H.now + (int64_t)kmin;
+        const bool tie = (k == kmin);
+        const uint64_t tied = __ballot(tie);
+        uint32_t win;
+        if ((tied & (tied - 1)) == 0) {
+            win = (uint32_t)__builtin_ctzll(tied);
+        } else {                                                    // same-ns events: ns-3 uid order
+            const uint32_t smin = wave_umin_fast(tie ? s : 0xffffffffu);
+            win = (uint32_t)__builtin_ctzll(__ballot(tie && s == smin));
+        }
+        bc = rdl(c, win);
+        return;
+    }
+    // every source is >= 2^32-1 ns away (or none is pending): exact 64-bit path
+    int64_t t = INT64_MAX;
+    uint32_t s2 = 0xffffffffu, c2 = 0xffffffffu;
 #pragma unroll
     for (int j = 0; j < FS; ++j) {
         int64_t tj = mk64(R.fk_lo.v[j], R.fk_hi.v[j]);
         uint32_t sj = R.fk_seq.v[j];
-        if (key_less(tj, sj, t, s)) { t = tj; s = sj; c = (K_FLOW << 28) | (uint32_t)(lane + 64 * j); }
+        if (key_less(tj, sj, t, s2)) { t = tj; s2 = sj; c2 = (K_FLOW << 28) | (uint32_t)(lane + 64 * j); }
     }
-#pragma unroll
-    for (int j = 0; j < LS; ++j) {
-        int64_t tj = mk64(R.lk_lo.v[j], R.lk_hi.v[j]);
-        uint32_t sj = R.lk_seq.v[j];
-        if (key_less(tj, sj, t, s)) { t = tj; s = sj; c = (R.lk_kind.v[j] << 28) | (uint32_t)(lane + 64 * j); }
-    }
-    if (lane == 0 && key_less(H.ping_t, H.ping_seq, t, s)) { t = H.ping_t; s = H.ping_seq; c = K_PING << 28; }
-    const uint64_t dt = (uint64_t)(t - H.now);
-    const uint32_t key = (dt >> 32) ? 0xffffffffu : (uint32_t)dt;
-    const uint32_t kmin = wave_umin_fast(key);
-    bool tie;
-    if (kmin != 0xffffffffu) {
-        bt = H.now + (int64_t)kmin;
-        tie = (key == kmin);
-    } else {
-        bt = wave_min_i64(t);
-        tie = (t == bt);
-    }
+    if (lane == 0 && key_less(H.ping_t, H.ping_seq, t, s2)) { t = H.ping_t; s2 = H.ping_seq; c2 = K_PING << 28; }
+    bt = wave_min_i64(t);
+    const bool tie = (t == bt);
     const uint64_t tied = __ballot(tie);
     uint32_t win;
     if ((tied & (tied - 1)) == 0) {
         win = (uint32_t)__builtin_ctzll(tied);
-    } else {                                                        // same-ns events: ns-3 uid order
-        uint32_t smin = wave_umin_fast(tie ? s : 0xffffffffu);
-        win = (uint32_t)__builtin_ctzll(__ballot(tie && s == smin));
+    } else {
+        const uint32_t smin = wave_umin_fast(tie ? s2 : 0xffffffffu);
+        win = (uint32_t)__builtin_ctzll(__ballot(tie && s2 == smin));
     }
-    bc = rdl(c, win);
+    bc = rdl(c2, win);
 }
 
 // ---------------------------------------------------------------------------
@@ -1037,6 +1069,11 @@ prisma_step_kernel_t(KParams P) {
     if (H.over || (table_mode && H.hops_launch >= max_hops)) H.stop = 1;
 
     uint32_t resets = 0;
+    // Drain the stage-in loads here: otherwise the waitcnt pass keeps them
+    // "possibly pending" at the loop header and emits vmcnt waits there that,
+    // on every later iteration, also wait for the previous event's record
+    // stores.
+    __builtin_amdgcn_s_waitcnt(0);
 #if PRISMA_TIMING
     uint64_t tm_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t tm_cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
