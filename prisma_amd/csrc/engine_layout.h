@@ -61,14 +61,27 @@ struct Hdr {                 // 128 bytes at state offset 0
     uint32_t pad[6];
 };
 static_assert(sizeof(Hdr) == 128, "Hdr size");
+// LDS offsets of the header, the counters (144 B) and the pending observation
+constexpr uint32_t kOffHdr = 0u, kOffCnt = 128u, kOffObs = 272u;
+
+// Read-only topology image (HBM, one per engine), fixed-size arrays so every
+// field sits at a compile-time offset from one base pointer: N <= 255,
+// links incl. access links <= 256, flows <= 512 (checked on the host).
+struct TopoImage {
+    int32_t rowptr[256];         // CSR of directed switch links by source node
+    int32_t ldst[256];           // far end of link l (access link E+u: u)
+    int32_t lrev[256];           // reverse switch link
+    int64_t acctx[256];          // access-link tx time of node u (ns)
+    int32_t fsrc[512];
+    int32_t fdst[512];
+    double  fmean[512];          // mean inter-arrival of flow f (s)
+};
 
 // Offsets (bytes) of every region; filled on the host, read by the kernels
 // from a device copy.
 struct Layout {
     int32_t N, E, L, F, W, max_deg, WCAP, MA;
     uint32_t topo_bytes, state_bytes, lds_bytes, table_bytes;
-    // topology image (HBM, read through the scalar cache)
-    uint32_t t_rowptr, t_ldst, t_lrev, t_acctx, t_fsrc, t_fdst, t_fmean;
     // state image (LDS offset 0) and the action table (LDS offset lds_state_bytes)
     uint32_t s_hdr, s_cnt, s_obs, s_wt, s_wseq, s_ring, s_win, s_pbd;
     uint32_t lds_state_bytes;    // LDS part of the image (bytes [0, lds_state_bytes))

@@ -238,7 +238,8 @@ struct Hot {
     int64_t  now, ping_t;
     uint32_t ping_seq, seq, uid, dec, ping_rounds, episode;
     uint32_t pend, over, error, stop, hops_launch;
-    uint64_t hops_total, events_total;
+    uint32_t ev_launch;          // events executed in this launch (the running
+                                 // totals stay in the LDS header until exit)
 };
 
 
@@ -250,9 +251,69 @@ typedef const CAS int64_t c_i64;
 typedef const CAS double c_f64;
 typedef const CAS Layout CLayout;        // scenario constants: s_load, never clobbered
 
+// Scenario constants in one VGPR: lane i holds dword i of the Layout, read
+// with v_readlane (25-cycle dependent latency on gfx950, measured by
+// scripts/ubench/latency.hip) instead of s_load through the scalar cache
+// (60 cycles) -- the compiler re-issued those loads inside the event loop
+// because the constants do not fit in SGPRs next to the replica state.
+static_assert(sizeof(Layout) <= 4 * kWave, "Layout must fit one VGPR");
+struct LV {
+    uint32_t w;
+    __device__ __forceinline__ void load(const Layout* lay, int lane) {
+        w = (lane < (int)(sizeof(Layout) / 4)) ? ((const uint32_t*)lay)[lane] : 0u;
+    }
+    __device__ __forceinline__ uint32_t u(int i) const { return (uint32_t)__builtin_amdgcn_readlane((int)w, i); }
+    __device__ __forceinline__ int32_t N() const { return (int32_t)u(offsetof(Layout, N) / 4); }
+    __device__ __forceinline__ int32_t E() const { return (int32_t)u(offsetof(Layout, E) / 4); }
+    __device__ __forceinline__ int32_t L() const { return (int32_t)u(offsetof(Layout, L) / 4); }
+    __device__ __forceinline__ int32_t F() const { return (int32_t)u(offsetof(Layout, F) / 4); }
+    __device__ __forceinline__ int32_t W() const { return (int32_t)u(offsetof(Layout, W) / 4); }
+    __device__ __forceinline__ int32_t max_deg() const { return (int32_t)u(offsetof(Layout, max_deg) / 4); }
+    __device__ __forceinline__ int32_t WCAP() const { return (int32_t)u(offsetof(Layout, WCAP) / 4); }
+    __device__ __forceinline__ int32_t MA() const { return (int32_t)u(offsetof(Layout, MA) / 4); }
+    __device__ __forceinline__ uint32_t topo_bytes() const { return (uint32_t)u(offsetof(Layout, topo_bytes) / 4); }
+    __device__ __forceinline__ uint32_t state_bytes() const { return (uint32_t)u(offsetof(Layout, state_bytes) / 4); }
+    __device__ __forceinline__ uint32_t lds_bytes() const { return (uint32_t)u(offsetof(Layout, lds_bytes) / 4); }
+    __device__ __forceinline__ uint32_t table_bytes() const { return (uint32_t)u(offsetof(Layout, table_bytes) / 4); }
+    __device__ __forceinline__ uint32_t s_hdr() const { return (uint32_t)u(offsetof(Layout, s_hdr) / 4); }
+    __device__ __forceinline__ uint32_t s_cnt() const { return (uint32_t)u(offsetof(Layout, s_cnt) / 4); }
+    __device__ __forceinline__ uint32_t s_obs() const { return (uint32_t)u(offsetof(Layout, s_obs) / 4); }
+    __device__ __forceinline__ uint32_t s_wt() const { return (uint32_t)u(offsetof(Layout, s_wt) / 4); }
+    __device__ __forceinline__ uint32_t s_wseq() const { return (uint32_t)u(offsetof(Layout, s_wseq) / 4); }
+    __device__ __forceinline__ uint32_t s_ring() const { return (uint32_t)u(offsetof(Layout, s_ring) / 4); }
+    __device__ __forceinline__ uint32_t s_win() const { return (uint32_t)u(offsetof(Layout, s_win) / 4); }
+    __device__ __forceinline__ uint32_t s_pbd() const { return (uint32_t)u(offsetof(Layout, s_pbd) / 4); }
+    __device__ __forceinline__ uint32_t lds_state_bytes() const { return (uint32_t)u(offsetof(Layout, lds_state_bytes) / 4); }
+    __device__ __forceinline__ uint32_t s_regs() const { return (uint32_t)u(offsetof(Layout, s_regs) / 4); }
+    __device__ __forceinline__ uint32_t PBK() const { return (uint32_t)u(offsetof(Layout, PBK) / 4); }
+    __device__ __forceinline__ int32_t FS() const { return (int32_t)u(offsetof(Layout, FS) / 4); }
+    __device__ __forceinline__ int32_t LS() const { return (int32_t)u(offsetof(Layout, LS) / 4); }
+    __device__ __forceinline__ int64_t sw_txd() const { return mk64(u(offsetof(Layout, sw_txd) / 4), u(offsetof(Layout, sw_txd) / 4 + 1)); }
+    __device__ __forceinline__ int64_t sw_txp() const { return mk64(u(offsetof(Layout, sw_txp) / 4), u(offsetof(Layout, sw_txp) / 4 + 1)); }
+    __device__ __forceinline__ int64_t sw_prop() const { return mk64(u(offsetof(Layout, sw_prop) / 4), u(offsetof(Layout, sw_prop) / 4 + 1)); }
+    __device__ __forceinline__ uint32_t qcap_s() const { return (uint32_t)u(offsetof(Layout, qcap_s) / 4); }
+    __device__ __forceinline__ uint32_t qcap_a() const { return (uint32_t)u(offsetof(Layout, qcap_a) / 4); }
+    __device__ __forceinline__ uint32_t qmax_bytes() const { return (uint32_t)u(offsetof(Layout, qmax_bytes) / 4); }
+    __device__ __forceinline__ uint32_t acc_qmax_pkts() const { return (uint32_t)u(offsetof(Layout, acc_qmax_pkts) / 4); }
+    __device__ __forceinline__ int64_t t_end() const { return mk64(u(offsetof(Layout, t_end) / 4), u(offsetof(Layout, t_end) / 4 + 1)); }
+    __device__ __forceinline__ int64_t ping_period() const { return mk64(u(offsetof(Layout, ping_period) / 4), u(offsetof(Layout, ping_period) / 4 + 1)); }
+    __device__ __forceinline__ uint32_t data_size() const { return (uint32_t)u(offsetof(Layout, data_size) / 4); }
+    __device__ __forceinline__ uint32_t ping_size() const { return (uint32_t)u(offsetof(Layout, ping_size) / 4); }
+    __device__ __forceinline__ uint32_t ma() const { return (uint32_t)u(offsetof(Layout, ma) / 4); }
+    __device__ __forceinline__ uint32_t ping_as_obs() const { return (uint32_t)u(offsetof(Layout, ping_as_obs) / 4); }
+    __device__ __forceinline__ uint32_t auto_reset() const { return (uint32_t)u(offsetof(Layout, auto_reset) / 4); }
+    __device__ __forceinline__ uint32_t seed_lo() const { return (uint32_t)u(offsetof(Layout, seed_lo) / 4); }
+    __device__ __forceinline__ uint32_t replica_base() const { return (uint32_t)u(offsetof(Layout, replica_base) / 4); }
+    __device__ __forceinline__ uint32_t log_cap() const { return (uint32_t)u(offsetof(Layout, log_cap) / 4); }
+    __device__ __forceinline__ uint32_t rec_bytes() const { return (uint32_t)u(offsetof(Layout, rec_bytes) / 4); }
+    __device__ __forceinline__ double loss_penalty() const { return __longlong_as_double(mk64(u(offsetof(Layout, loss_penalty) / 4), u(offsetof(Layout, loss_penalty) / 4 + 1))); }
+    __device__ __forceinline__ float loss_penalty_f() const { return __uint_as_float(u(offsetof(Layout, loss_penalty_f) / 4)); }
+};
+
+
 // LDS views of one replica + its topology
 struct Sim {
-    CLayout* L;
+    LV lv;                                  // scenario constants (one VGPR)
     unsigned char* base;
     Hdr* h;
     prisma_counters_t* c;
@@ -261,35 +322,30 @@ struct Sim {
     uint32_t* ring;
     float* win;
     float* pbd;                             // ping-back delays [E][PBK]
-    c_i32* rowptr; c_i32* ldst; c_i32* lrev;
-    c_i64* acctx;
-    c_i32* fsrc; c_i32* fdst; c_f64* fmean;
+    const CAS TopoImage* T;                 // topology (scalar loads at fixed offsets)
     const uint8_t* table;
     unsigned char* logrep;
     uint32_t gid;
     int lane;
+#if PRISMA_TIMING
+    mutable uint64_t tsub[2], tlast;             // sub-phase cycles inside apply_decision
+#endif
 };
 
-__device__ inline void sim_bind(Sim& S, CLayout& L, unsigned char* lds, const unsigned char* topo,
+__device__ inline void sim_bind(Sim& S, const LV& L, unsigned char* lds, const unsigned char* topo,
                                 unsigned char* logrep, uint32_t gid, int lane) {
-    S.L = &L;
+    S.lv = L;
     S.base = lds;
-    S.h = (Hdr*)(lds + L.s_hdr);
-    S.c = (prisma_counters_t*)(lds + L.s_cnt);
-    S.obs = (uint32_t*)(lds + L.s_obs);
-    S.wt = (uint32_t*)(lds + L.s_wt);
-    S.wseq = (uint32_t*)(lds + L.s_wseq);
-    S.ring = (uint32_t*)(lds + L.s_ring);
-    S.win = (float*)(lds + L.s_win);
-    S.pbd = (float*)(lds + L.s_pbd);
-    S.rowptr = (c_i32*)(topo + L.t_rowptr);
-    S.ldst = (c_i32*)(topo + L.t_ldst);
-    S.lrev = (c_i32*)(topo + L.t_lrev);
-    S.acctx = (c_i64*)(topo + L.t_acctx);
-    S.fsrc = (c_i32*)(topo + L.t_fsrc);
-    S.fdst = (c_i32*)(topo + L.t_fdst);
-    S.fmean = (c_f64*)(topo + L.t_fmean);
-    S.table = (const uint8_t*)(lds + L.lds_state_bytes);
+    S.h = (Hdr*)(lds + kOffHdr);                // fixed offsets (asserted in build_layout)
+    S.c = (prisma_counters_t*)(lds + kOffCnt);
+    S.obs = (uint32_t*)(lds + kOffObs);
+    S.wt = (uint32_t*)(lds + L.s_wt());
+    S.wseq = (uint32_t*)(lds + L.s_wseq());
+    S.ring = (uint32_t*)(lds + L.s_ring());
+    S.win = (float*)(lds + L.s_win());
+    S.pbd = (float*)(lds + L.s_pbd());
+    S.T = (const CAS TopoImage*)topo;
+    S.table = (const uint8_t*)(lds + L.lds_state_bytes());
     S.logrep = logrep;
     S.gid = gid;
     S.lane = lane;
@@ -315,8 +371,7 @@ __device__ inline void hot_load(const Sim& S, Hot& H) {
     H.dec = u_ld32(&h.dec_count); H.ping_rounds = u_ld32(&h.ping_rounds); H.episode = u_ld32(&h.episode);
     H.pend = u_ld32(&h.pend); H.over = u_ld32(&h.over); H.error = u_ld32(&h.error);
     H.stop = u_ld32(&h.stop); H.hops_launch = u_ld32(&h.hops_launch);
-    H.hops_total = (uint64_t)u_ld64((const int64_t*)&h.hops_total);
-    H.events_total = (uint64_t)u_ld64((const int64_t*)&h.events_total);
+    H.ev_launch = 0;
 }
 
 template <int FS, int LS>
@@ -327,11 +382,11 @@ __device__ inline void hot_store(Sim& S, const Regs<FS, LS>& R, const Hot& H) {
         h.now = H.now; h.ping_t = H.ping_t; h.ping_seq = H.ping_seq; h.seq = H.seq; h.uid = H.uid;
         h.dec_count = H.dec; h.ping_rounds = H.ping_rounds; h.episode = H.episode; h.pend = H.pend;
         h.over = H.over; h.error = H.error; h.stop = H.stop; h.hops_launch = H.hops_launch;
-        h.hops_total = H.hops_total; h.events_total = H.events_total;
+        h.hops_total += H.hops_launch; h.events_total += H.ev_launch;
         prisma_counters_t& c = *S.c;
         c.now_ns = H.now; c.episode = H.episode; c.ping_rounds = H.ping_rounds; c.seq = H.seq; c.uid = H.uid;
         c.dec_count = H.dec; c.error = H.error; c.episode_over = H.over;
-        c.hops_total = H.hops_total; c.events_total = H.events_total;
+        c.hops_total = h.hops_total; c.events_total = h.events_total;
     }
 }
 
@@ -345,13 +400,13 @@ __device__ __forceinline__ bool key_less(int64_t t, uint32_t s, int64_t bt, uint
     return t < bt || (t == bt && s < bs);
 }
 
-__device__ __forceinline__ uint32_t ent_size(CLayout& L, uint32_t x) {
-    return ent_is_data(x) ? L.data_size : L.ping_size;
+__device__ __forceinline__ uint32_t ent_size(const LV& L, uint32_t x) {
+    return ent_is_data(x) ? L.data_size() : L.ping_size();
 }
-__device__ __forceinline__ uint32_t ring_off(CLayout& L, uint32_t l) {
-    return l < (uint32_t)L.E ? l * L.qcap_s : (uint32_t)L.E * L.qcap_s + (l - (uint32_t)L.E) * L.qcap_a;
+__device__ __forceinline__ uint32_t ring_off(const LV& L, uint32_t l) {
+    return l < (uint32_t)L.E() ? l * L.qcap_s() : (uint32_t)L.E() * L.qcap_s() + (l - (uint32_t)L.E()) * L.qcap_a();
 }
-__device__ __forceinline__ uint32_t ring_cap(CLayout& L, uint32_t l) { return l < (uint32_t)L.E ? L.qcap_s : L.qcap_a; }
+__device__ __forceinline__ uint32_t ring_cap(const LV& L, uint32_t l) { return l < (uint32_t)L.E() ? L.qcap_s() : L.qcap_a(); }
 
 // one link's fields as uniform scalars
 struct LinkV {
@@ -402,28 +457,28 @@ __device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, const Ho
 // ---- link FIFO / transmitter (point-to-point-net-device.cc:273-336, 595-666)
 __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l, LinkV& k, uint32_t ring_idx,
                                                uint32_t x) {
-    CLayout& L = *S.L;
-    const bool sw = l < (uint32_t)L.E;
-    int64_t tx = sw ? (ent_is_data(x) ? L.sw_txd : L.sw_txp) : S.acctx[l - (uint32_t)L.E];
-    int64_t prop = sw ? L.sw_prop : 0;
+    const LV& L = S.lv;
+    const bool sw = l < (uint32_t)L.E();
+    int64_t tx = sw ? (ent_is_data(x) ? L.sw_txd() : L.sw_txp()) : S.T->acctx[l - (uint32_t)L.E()];
+    int64_t prop = sw ? L.sw_prop() : 0;
     k.busy = 1;
     k.cp_t = lo32(H.now + tx);
     k.cp_seq = H.seq++;                                        // TransmitComplete
-    uint32_t w = l * (uint32_t)L.WCAP + (ring_idx & (uint32_t)(L.WCAP - 1));
+    uint32_t w = l * (uint32_t)L.WCAP() + (ring_idx & (uint32_t)(L.WCAP() - 1));
     const uint32_t at = lo32(H.now + tx + prop);
     const uint32_t as = H.seq++;                               // channel Receive
     if (S.lane == 0) { S.wt[w] = at; S.wseq[w] = as; }
     if (k.n_wire == 1) { k.wh_t = at; k.wh_seq = as; }        // the wire was empty: new head
-    if (k.n_wire > (uint32_t)L.WCAP) fail(H, PRISMA_EBIT_WIRE);
+    if (k.n_wire > (uint32_t)L.WCAP()) fail(H, PRISMA_EBIT_WIRE);
 }
 
 // returns 1 if enqueued, 0 if dropped (a ring overflow fails the replica)
 template <int FS, int LS>
 __device__ __forceinline__ int link_send(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, uint32_t e) {
-    CLayout& L = *S.L;
+    const LV& L = S.lv;
     LinkV k = link_get(R, l);
     uint32_t size = ent_size(L, e);
-    bool ok = l < (uint32_t)L.E ? (k.qb + size <= L.qmax_bytes) : (k.n_queue + 1u <= L.acc_qmax_pkts);
+    bool ok = l < (uint32_t)L.E() ? (k.qb + size <= L.qmax_bytes()) : (k.n_queue + 1u <= L.acc_qmax_pkts());
     if (!ok) return 0;
     uint32_t cap = ring_cap(L, l), off = ring_off(L, l);
     if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
@@ -446,7 +501,7 @@ __device__ __forceinline__ int link_send(const Sim& S, Regs<FS, LS>& R, Hot& H, 
 
 template <int FS, int LS>
 __device__ __forceinline__ void on_complete(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l) {   // :305-336
-    CLayout& L = *S.L;
+    const LV& L = S.lv;
     LinkV k = link_get(R, l);
     k.busy = 0;
     if (k.n_queue) {
@@ -465,8 +520,8 @@ __device__ __forceinline__ void on_complete(const Sim& S, Regs<FS, LS>& R, Hot& 
 // ---- observation (data-packet-manager.cc:171-206)
 // send time in seconds of ping round k as the ping-back manager stores it:
 // (double)GetMilliSeconds() * 0.001 (ping-back-packet-manager.cc:98-116)
-__device__ __forceinline__ double ping_send_s(CLayout& L, int64_t k) {
-    uint64_t ms = (uint64_t)(((k + 1) * L.ping_period) / 1000000);
+__device__ __forceinline__ double ping_send_s(const LV& L, int64_t k) {
+    uint64_t ms = (uint64_t)(((k + 1) * L.ping_period()) / 1000000);
     return (double)ms * 0.001;
 }
 
@@ -499,14 +554,14 @@ template <int FS, int LS>
 __device__ __forceinline__ uint32_t observe_links(const Sim& S, const Regs<FS, LS>& R, const Hot& H, uint32_t v,
                                                   double now_s) {
     if (PRISMA_ABLATE & 4) return 0u;
-    const int r0 = S.rowptr[v], deg = S.rowptr[v + 1] - r0;
+    const int r0 = S.T->rowptr[v], deg = S.T->rowptr[v + 1] - r0;
     const int lane = S.lane;
     const uint32_t src = (uint32_t)(r0 + lane - 1);
     uint32_t o = 0;
 #pragma unroll
     for (int j = 0; j < LS; ++j) {
         uint32_t val;
-        if (S.L->ping_as_obs)
+        if (S.lv.ping_as_obs())
             val = ping_value_lane(ld_d(R.pav_lo.v[j], R.pav_hi.v[j]), (int32_t)R.pm_hole.v[j], (int32_t)R.pm_ack.v[j],
                                   ld_d(R.hd_lo.v[j], R.hd_hi.v[j]), ld_d(R.nd_lo.v[j], R.nd_hi.v[j]), H.ping_rounds,
                                   now_s);
@@ -539,14 +594,14 @@ __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_
     }
     uint32_t ob = (uint32_t)__shfl((int)obs_reg, (lane - 8) & 63);
     uint32_t word = lane < 8 ? hw : ob;
-    uint32_t* p = (uint32_t*)(S.logrep + (size_t)(d & (S.L->log_cap - 1)) * S.L->rec_bytes);
-    if (lane < 8 + S.L->W) p[lane] = word;
+    uint32_t* p = (uint32_t*)(S.logrep + (size_t)(d & (S.lv.log_cap() - 1)) * S.lv.rec_bytes());
+    if (lane < 8 + S.lv.W()) p[lane] = word;
 }
 
 __device__ __forceinline__ void patch_record(const Sim& S, const Hot& H, uint32_t d, int action, uint32_t status) {
     if (PRISMA_ABLATE & 2) return;
     if (S.lane == 0) {
-        unsigned char* p = S.logrep + (size_t)(d & (S.L->log_cap - 1)) * S.L->rec_bytes;
+        unsigned char* p = S.logrep + (size_t)(d & (S.lv.log_cap() - 1)) * S.lv.rec_bytes();
         *(uint32_t*)(p + 28) = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
     }
 }
@@ -556,7 +611,7 @@ __device__ __forceinline__ void patch_record(const Sim& S, const Hot& H, uint32_
 template <int FS, int LS>
 __device__ __forceinline__ void receive_counters(const Sim& S, Regs<FS, LS>& R, const Hot& H, uint32_t x, bool arrived,
                                                  uint32_t start) {
-    CLayout& L = *S.L;
+    const LV& L = S.lv;
     if (arrived) {
         // valable, nextHop == finalDest on identity overlays
         R.cv.template add_u32<C_OV_ARR>(1u);
@@ -567,10 +622,10 @@ __device__ __forceinline__ void receive_counters(const Sim& S, Regs<FS, LS>& R, 
         R.cv.template add_u32<C_E2E_N>(1u);
     }
     // pings are always addressed to the node that receives them
-    if (!ent_is_data(x)) R.cv.template add_u32<C_BYTES_SIG>(L.ping_size - 2u);
+    if (!ent_is_data(x)) R.cv.template add_u32<C_BYTES_SIG>(L.ping_size() - 2u);
     if (ent_type(x) == T_FRESH) {
         R.cv.template add_u32<C_OV_INJ>(1u);
-        R.cv.template add_u32<C_BYTES_DATA>(L.data_size - 2u);
+        R.cv.template add_u32<C_BYTES_DATA>(L.data_size() - 2u);
     }
 }
 
@@ -582,8 +637,11 @@ template <int FS, int LS>
 __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t x, uint32_t dst,
                                                uint32_t start, uint32_t uid, uint32_t v, uint32_t d, int action,
                                                bool fused, double reward, int32_t prev, uint32_t obs_reg) {
-    CLayout& L = *S.L;
-    int r0 = S.rowptr[v], deg = S.rowptr[v + 1] - r0;
+    const LV& L = S.lv;
+#if PRISMA_TIMING
+    S.tlast = TM_NOW();
+#endif
+    int r0 = S.T->rowptr[v], deg = S.T->rowptr[v + 1] - r0;
     uint32_t status;
     if (action >= 0 && action < deg) {
         uint32_t l = (uint32_t)(r0 + action);
@@ -595,16 +653,22 @@ __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Ho
         } else {
             status = PRISMA_ST_DROPPED;              // :655-664 + forwarder.py:214-244
             R.cv.template add_u32<C_OV_LOST>(1u);
-            R.cv.template add_f32<C_COST>(L.loss_penalty_f);
+            R.cv.template add_f32<C_COST>(L.loss_penalty_f());
             R.cv.template add_u32<C_COST_N>(1u);
-            R.cv.template add_f64<C_REWARD>(L.loss_penalty);
+            R.cv.template add_f64<C_REWARD>(L.loss_penalty());
         }
     } else {
         status = PRISMA_ST_DISCARDED;
     }
+#if PRISMA_TIMING
+    { const uint64_t t = TM_NOW(); S.tsub[0] += t - S.tlast; S.tlast = t; }
+#endif
     if (fused) write_record(S, H, d, reward, uid, prev, v, dst, start, action, status, obs_reg);
     else patch_record(S, H, d, action, status);
     receive_counters(S, R, H, x, false, 0u);
+#if PRISMA_TIMING
+    { const uint64_t t = TM_NOW(); S.tsub[1] += t - S.tlast; S.tlast = t; }
+#endif
 }
 
 template <int FS, int LS>
@@ -618,11 +682,11 @@ __device__ __forceinline__ void finish_pending(const Sim& S, Regs<FS, LS>& R, Ho
 // ---- handlers (uniform) ------------------------------------------------------
 template <int FS, int LS>
 __device__ __forceinline__ void on_ping_round(const Sim& S, Regs<FS, LS>& R, Hot& H) {   // data-packet-manager.cc:350-413
-    CLayout& L = *S.L;
+    const LV& L = S.lv;
     uint32_t k = H.ping_rounds;
     uint32_t first_rearm = 0;
-    for (int u = 0; u < L.N; ++u) {
-        int r0 = S.rowptr[u], r1 = S.rowptr[u + 1];
+    for (int u = 0; u < L.N(); ++u) {
+        int r0 = S.T->rowptr[u], r1 = S.T->rowptr[u + 1];
         for (int l = r0; l < r1; ++l) {
             if (!link_send(S, R, H, (uint32_t)l, p_make(T_PFWD, (uint32_t)(l - r0), k))) R.cv.template add_u32<C_CTRL_DROP>(1u);
         }
@@ -631,19 +695,19 @@ __device__ __forceinline__ void on_ping_round(const Sim& S, Regs<FS, LS>& R, Hot
     }
     H.ping_rounds = k + 1;
     // one ns-3 event per node timer (the round is N consecutive events)
-    R.cv.template add_u64<C_EVENTS>((uint64_t)(L.N - 1));
-    H.events_total += (uint64_t)(L.N - 1);
-    H.ping_t = H.now + L.ping_period;
+    R.cv.template add_u64<C_EVENTS>((uint64_t)(L.N() - 1));
+    H.ev_launch += (uint32_t)(L.N() - 1);
+    H.ping_t = H.now + L.ping_period();
     H.ping_seq = first_rearm;
 }
 
 template <int FS, int LS>
 __device__ __forceinline__ void flow_next(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t f, uint32_t draw) {
     uint32_t c[4] = { f, draw, H.episode, 1u };                   // poisson-application.cc:265-295
-    philox4x32_10(c, S.L->seed_lo, S.gid);
+    philox4x32_10(c, S.lv.seed_lo(), S.gid);
     uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
     double U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
-    double delay = -S.fmean[f] * det_log(U);
+    double delay = -S.T->fmean[f] * det_log(U);
     int64_t t = H.now + sec_to_ns(delay);
     R.fk_lo.set(f, lo32(t));
     R.fk_hi.set(f, hi32(t));
@@ -655,9 +719,9 @@ template <int FS, int LS>
 __device__ __forceinline__ void on_flow(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t f) {
     uint32_t draw = R.f_draw.get(f);
     if (draw != 0) {                                                // SendPacket :297-358
-        uint32_t src = (uint32_t)S.fsrc[f];
+        uint32_t src = (uint32_t)S.T->fsrc[f];
         uint32_t par = (uint32_t)(H.now / 1000000000) & 1u;         // start second (its parity)
-        link_send(S, R, H, (uint32_t)S.L->E + src, f_make(f, par, H.uid & kUidMask));   // access link
+        link_send(S, R, H, (uint32_t)S.lv.E() + src, f_make(f, par, H.uid & kUidMask));   // access link
         H.uid++;
     }
     flow_next(S, R, H, f, draw);                                    // StartSending / ScheduleNextTx
@@ -666,12 +730,12 @@ __device__ __forceinline__ void on_flow(const Sim& S, Regs<FS, LS>& R, Hot& H, u
 // the head packet leaves the wire of link l (arrival at the far end)
 template <int FS, int LS>
 __device__ __forceinline__ void wire_pop(const Sim& S, Regs<FS, LS>& R, const Hot& H, uint32_t l, LinkV& k) {
-    CLayout& L = *S.L;
+    const LV& L = S.lv;
     const uint32_t cap = ring_cap(L, l);
     k.head = (k.head + 1 == cap) ? 0 : k.head + 1;
     k.n_wire--;
     if (k.n_wire) {                                                 // next packet on the wire
-        const uint32_t w = l * (uint32_t)L.WCAP + (k.head & (uint32_t)(L.WCAP - 1));
+        const uint32_t w = l * (uint32_t)L.WCAP() + (k.head & (uint32_t)(L.WCAP() - 1));
         k.wh_t = u_ld32(S.wt + w);
         k.wh_seq = u_ld32(S.wseq + w);
     }
@@ -685,11 +749,11 @@ struct Decision {
 // returns 1 if a data decision needs an action
 template <int FS, int LS>
 __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, Decision& D, bool fused) {
-    CLayout& L = *S.L;
+    const LV& L = S.lv;
     LinkV k = link_get(R, l);
     const uint32_t x = u_ld32(&S.ring[ring_off(L, l) + k.head]);
     const uint32_t type = ent_type(x);
-    const uint32_t v = (uint32_t)S.ldst[l];
+    const uint32_t v = (uint32_t)S.T->ldst[l];
     if (ent_is_data(x)) {
         // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
         // A forwarded packet's previous decision record (t_ns, uid, dst,
@@ -702,7 +766,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
         // load and its consumption are unconditional on this path.)
         const uint32_t d = H.dec;
         const uint32_t dist = (d - r_dec(x)) & kRelayMask;
-        const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap - 1)) * L.rec_bytes;
+        const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap() - 1)) * L.rec_bytes();
         const uint4 ph = *(const uint4*)pr;
         const uint32_t w6 = *(const uint32_t*)(pr + 24);
         wire_pop(S, R, H, l, k);
@@ -718,7 +782,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             // second rebuilt from their low bits (the packet left its app less
             // than 1 s and fewer than 2^20 injections ago)
             const uint32_t f = f_flow(x);
-            dst = (uint32_t)S.fdst[f];
+            dst = (uint32_t)S.T->fdst[f];
             const uint32_t s0 = (uint32_t)(H.now / 1000000000);
             start = s0 - ((s0 ^ f_parity(x)) & 1u);
             const uint32_t last = H.uid - 1u;
@@ -727,7 +791,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             dst = (x >> 2) & 255u; start = x >> 10; uid = 0; prev = (int32_t)d - 1;
         } else {
             prev = (int32_t)(d - dist);
-            if (dist >= L.log_cap) fail(H, PRISMA_EBIT_LOGWRAP);
+            if (dist >= L.log_cap()) fail(H, PRISMA_EBIT_LOGWRAP);
             uid = uid_prev;
             dst = (w_prev >> 8) & 255u;
             start = w_prev >> 16;
@@ -750,11 +814,11 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     const uint32_t tun = p_tunnel(x), rnd = p_round(x);
     if (type == T_PFWD) {                                           // ping-forward-packet-manager.cc:94-156
         float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
-        if (S.lane == 0) S.pbd[l * L.PBK + (rnd & (L.PBK - 1))] = delay;
-        if (!link_send(S, R, H, (uint32_t)S.lrev[l], p_make(T_PBACK, tun, rnd))) R.cv.template add_u32<C_CTRL_DROP>(1u);
+        if (S.lane == 0) S.pbd[l * L.PBK() + (rnd & (L.PBK() - 1))] = delay;
+        if (!link_send(S, R, H, (uint32_t)S.T->lrev[l], p_make(T_PBACK, tun, rnd))) R.cv.template add_u32<C_CTRL_DROP>(1u);
     } else {                                                        // ping-back-packet-manager.cc:120-144
-        const uint32_t lt = (uint32_t)S.rowptr[v] + tun;
-        const float delay = __uint_as_float(u_ld32((const uint32_t*)S.pbd + lt * L.PBK + (rnd & (L.PBK - 1))));
+        const uint32_t lt = (uint32_t)S.T->rowptr[v] + tun;
+        const float delay = __uint_as_float(u_ld32((const uint32_t*)S.pbd + lt * L.PBK() + (rnd & (L.PBK() - 1))));
         int32_t acked = (int32_t)R.pm_ack.get(lt), hole = (int32_t)R.pm_hole.get(lt);
         int32_t idx = (int32_t)rnd;
         if (idx <= acked) {
@@ -771,7 +835,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             R.nd_lo.set(lt, (uint32_t)nd);
             R.nd_hi.set(lt, (uint32_t)(nd >> 32));
         }
-        uint32_t MA = L.ma;
+        uint32_t MA = L.ma();
         uint32_t pw = R.pm_win.get(lt);
         uint32_t wn = pw & 0xffffu, wh = pw >> 16, slot;
         if (wn >= MA) {
@@ -803,15 +867,17 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
 // ---------------------------------------------------------------------------
 // replica (re)initialisation: LDS image zeroed, registers set (all lanes)
 // ---------------------------------------------------------------------------
+// keep_totals: carry the header's hops_total / events_total over (auto-reset)
 template <int FS, int LS>
-__device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t episode) {
-    CLayout& L = *S.L;
+__device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t episode, bool keep_totals) {
+    const LV& L = S.lv;
     const int lane = S.lane;
-    uint32_t dec = H.dec, hl = H.hops_launch;
-    uint64_t ht = H.hops_total, et = H.events_total;
+    uint32_t dec = H.dec, hl = H.hops_launch, el = H.ev_launch;
+    const uint64_t ht = keep_totals ? (uint64_t)u_ld64((const int64_t*)&S.h->hops_total) : 0u;
+    const uint64_t et = keep_totals ? (uint64_t)u_ld64((const int64_t*)&S.h->events_total) : 0u;
     __syncthreads();
     uint4* st4 = (uint4*)S.base;
-    for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
+    for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes() / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
     R.cv.lo = 0;
     R.cv.hi = 0;
 #pragma unroll
@@ -819,13 +885,13 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
         uint32_t f = (uint32_t)lane + 64u * j;
         int64_t t = INT64_MAX;
         uint32_t s = 0xffffffffu;
-        if (f < (uint32_t)L.F) {
+        if (f < (uint32_t)L.F()) {
             uint32_t c[4] = { f, 0u, episode, 0u };
-            philox4x32_10(c, L.seed_lo, S.gid);
+            philox4x32_10(c, L.seed_lo(), S.gid);
             uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
             double U = (double)u53 * (1.0 / 9007199254740992.0);
             t = sec_to_ns(0.0001 + U);                              // sim.cc:610-630
-            s = (uint32_t)L.N + f;
+            s = (uint32_t)L.N() + f;
         }
         R.fk_lo.v[j] = lo32(t); R.fk_hi.v[j] = hi32(t); R.fk_seq.v[j] = s; R.f_draw.v[j] = 0;
     }
@@ -841,13 +907,17 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
         R.hd_lo.v[j] = 0; R.hd_hi.v[j] = 0;
     }
     H.now = 0;
-    H.ping_t = L.ping_period;                                       // data-packet-manager.cc:118-121
+    H.ping_t = L.ping_period();                                       // data-packet-manager.cc:118-121
     H.ping_seq = 0;
-    H.seq = (uint32_t)L.N + (uint32_t)L.F;
+    H.seq = (uint32_t)L.N() + (uint32_t)L.F();
     H.uid = 0; H.ping_rounds = 0; H.pend = 0; H.over = 0; H.error = 0; H.stop = 0;
-    H.dec = dec; H.hops_launch = hl; H.hops_total = ht; H.events_total = et;
+    H.dec = dec; H.hops_launch = hl; H.ev_launch = el;
     H.episode = episode;
-    if (lane == 0) S.c->episode = episode;
+    if (lane == 0) {
+        S.c->episode = episode;
+        S.h->hops_total = ht;
+        S.h->events_total = et;
+    }
     __syncthreads();
 }
 
@@ -975,33 +1045,33 @@ __device__ __forceinline__ void select_event(const Regs<FS, LS>& R, const Hot& H
 // ---------------------------------------------------------------------------
 // the [N][N] action table (table policy) sits in LDS after the state image
 __device__ __forceinline__ void stage_table(unsigned char* lds, const KParams& P, int lane) {
-    CLayout& L = *(CLayout*)P.lay;
+    CLayout& LC = *(CLayout*)P.lay;
     if (P.table) {
-        uint8_t* dstp = lds + L.lds_state_bytes;
-        const uint32_t nt = (uint32_t)(L.N * L.N);
+        uint8_t* dstp = lds + LC.lds_state_bytes;
+        const uint32_t nt = (uint32_t)(LC.N * LC.N);
         for (uint32_t i = (uint32_t)lane; i < nt; i += kWave) dstp[i] = P.table[i];
     }
 }
 
 template <int FS, int LS>
 __device__ __forceinline__ void stage_in(unsigned char* lds, const KParams& P, int r, int lane, Regs<FS, LS>& R) {
-    CLayout& L = *(CLayout*)P.lay;
+    CLayout& LC = *(CLayout*)P.lay;
     stage_table(lds, P, lane);
-    const unsigned char* img = P.state + (size_t)r * L.state_bytes;
+    const unsigned char* img = P.state + (size_t)r * LC.state_bytes;
     const uint4* s4 = (const uint4*)img;
     uint4* d4 = (uint4*)lds;
-    for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes / 16u; i += kWave) d4[i] = s4[i];
-    regs_io(R, (uint32_t*)(const_cast<unsigned char*>(img) + L.s_regs), lane, false);
+    for (uint32_t i = (uint32_t)lane; i < LC.lds_state_bytes / 16u; i += kWave) d4[i] = s4[i];
+    regs_io(R, (uint32_t*)(const_cast<unsigned char*>(img) + LC.s_regs), lane, false);
 }
 
 template <int FS, int LS>
 __device__ __forceinline__ void stage_out(unsigned char* lds, const KParams& P, int r, int lane, Regs<FS, LS>& R) {
-    CLayout& L = *(CLayout*)P.lay;
-    unsigned char* img = P.state + (size_t)r * L.state_bytes;
+    CLayout& LC = *(CLayout*)P.lay;
+    unsigned char* img = P.state + (size_t)r * LC.state_bytes;
     uint4* s4 = (uint4*)img;
     const uint4* d4 = (const uint4*)lds;
-    for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes / 16u; i += kWave) s4[i] = d4[i];
-    regs_io(R, (uint32_t*)(img + L.s_regs), lane, true);
+    for (uint32_t i = (uint32_t)lane; i < LC.lds_state_bytes / 16u; i += kWave) s4[i] = d4[i];
+    regs_io(R, (uint32_t*)(img + LC.s_regs), lane, true);
 }
 
 __device__ __forceinline__ void publish_counters(const Sim& S, const KParams& P, int r, int lane) {
@@ -1014,13 +1084,15 @@ template <int FS, int LS>
 __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
-    CLayout& L = *(CLayout*)P.lay;
+    CLayout& LC = *(CLayout*)P.lay;
+    LV lv;
+    lv.load(P.lay, lane);
     Sim S;
-    sim_bind(S, L, lds, P.topo, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r, lane);
+    sim_bind(S, lv, lds, P.topo, P.log + (size_t)r * LC.log_cap * LC.rec_bytes, LC.replica_base + (uint32_t)r, lane);
     Regs<FS, LS> R;
     Hot H;
     memset(&H, 0, sizeof(H));
-    init_replica(S, R, H, P.episode);
+    init_replica(S, R, H, P.episode, false);
     hot_store(S, R, H);
     __syncthreads();
     publish_counters(S, P, r, lane);
@@ -1039,15 +1111,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(StepOcc
 prisma_step_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
-    CLayout& L = *(CLayout*)P.lay;
+    CLayout& LC = *(CLayout*)P.lay;
+    LV lv;
+    lv.load(P.lay, lane);
     Regs<FS, LS> R;
     stage_in(lds, P, r, lane, R);
     __syncthreads();
     Sim S;
-    sim_bind(S, L, lds, P.topo, P.log + (size_t)r * L.log_cap * L.rec_bytes, L.replica_base + (uint32_t)r, lane);
+    sim_bind(S, lv, lds, P.topo, P.log + (size_t)r * LC.log_cap * LC.rec_bytes, LC.replica_base + (uint32_t)r, lane);
+    const LV& L = S.lv;
     const bool table_mode = (P.mode == 2);
     const uint32_t max_hops = (uint32_t)P.max_hops;
-    const uint32_t NN = (uint32_t)L.N;
+    const uint32_t NN = (uint32_t)L.N();
     Hot H;
     hot_load(S, H);
     R.cv.load(S.c, (uint32_t)lane);
@@ -1059,7 +1134,6 @@ prisma_step_kernel_t(KParams P) {
             uint32_t pn = u_ld32(&S.h->pend_node), pd = u_ld32(&S.h->pend_ent[1]);
             finish_pending(S, R, H, (int)rfl((uint32_t)S.table[pn * NN + pd]));
             H.hops_launch++;
-            H.hops_total++;
         } else if (P.actions) {
             finish_pending(S, R, H, (int)rfl((uint32_t)P.actions[r]));
         } else {
@@ -1078,6 +1152,7 @@ prisma_step_kernel_t(KParams P) {
     uint64_t tm_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t tm_cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tm_a = 0, tm_b = 0;
+    S.tsub[0] = 0; S.tsub[1] = 0; S.tlast = 0;
 #define TM_MARK(i) do { tm_b = TM_NOW(); tm_acc[i] += tm_b - tm_a; tm_cnt[i]++; tm_a = tm_b; } while (0)
 #else
 #define TM_MARK(i) do { } while (0)
@@ -1089,10 +1164,10 @@ prisma_step_kernel_t(KParams P) {
         tm_a = TM_NOW();
 #endif
         select_event(R, H, lane, bt, bc);
-        if (bt >= L.t_end) {                           // Simulator::Stop(simTime) (sim.cc:703)
-            if (L.auto_reset && resets < 64u) {        // bounded: an empty scenario cannot spin forever
+        if (bt >= L.t_end()) {                           // Simulator::Stop(simTime) (sim.cc:703)
+            if (L.auto_reset() && resets < 64u) {        // bounded: an empty scenario cannot spin forever
                 ++resets;
-                init_replica(S, R, H, H.episode + 1u);
+                init_replica(S, R, H, H.episode + 1u, true);
                 continue;
             }
             H.over = 1;
@@ -1101,7 +1176,7 @@ prisma_step_kernel_t(KParams P) {
         }
         H.now = bt;
         R.cv.template add_u64<C_EVENTS>(1u);
-        H.events_total++;
+        H.ev_launch++;
         const uint32_t kind = bc >> 28, id = bc & 0x0fffffffu;
         TM_MARK(0);
         if (kind == K_ARRIVE) {
@@ -1114,7 +1189,6 @@ prisma_step_kernel_t(KParams P) {
                     apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, (int)rfl((uint32_t)a), true,
                                    D.reward, D.prev, D.obs);
                     H.hops_launch++;
-                    H.hops_total++;
                     if (H.hops_launch >= max_hops) H.stop = 1;
                     TM_MARK(2);
                 } else {
@@ -1123,7 +1197,7 @@ prisma_step_kernel_t(KParams P) {
                         h.pend_link = id; h.pend_node = D.v; h.pend_dec = D.d;
                         h.pend_ent[0] = D.x; h.pend_ent[1] = D.dst;
                     }
-                    if (lane < L.W) S.obs[lane] = D.obs;
+                    if (lane < L.W()) S.obs[lane] = D.obs;
                     H.pend = 1;
                     H.stop = 1;
                 }
@@ -1141,6 +1215,7 @@ prisma_step_kernel_t(KParams P) {
         if (H.error) { H.over = 1; H.stop = 1; }
     }
 #if PRISMA_TIMING
+    tm_acc[6] = S.tsub[0]; tm_acc[7] = S.tsub[1];
     if (lane == 0) {
         for (int i = 0; i < 8; ++i) {
             atomicAdd(&g_prisma_timing[i], (unsigned long long)tm_acc[i]);
@@ -1154,7 +1229,7 @@ prisma_step_kernel_t(KParams P) {
     const bool pending = H.pend && !H.over;
     if (P.mask_out && lane == 0) P.mask_out[r] = pending ? 1 : 0;
     if (P.node_out && lane == 0) P.node_out[r] = pending ? (int32_t)S.h->pend_node : -1;
-    if (P.obs_out && lane < L.W) P.obs_out[(size_t)r * L.W + lane] = pending ? (int32_t)S.obs[lane] : 0;
+    if (P.obs_out && lane < L.W()) P.obs_out[(size_t)r * L.W() + lane] = pending ? (int32_t)S.obs[lane] : 0;
     publish_counters(S, P, r, lane);
     stage_out(lds, P, r, lane, R);
 }
@@ -1317,26 +1392,19 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     // topology image
     uint32_t o = 0;
     auto take = [&](uint32_t bytes) { uint32_t r = o; o = align16(o + bytes); return r; };
-    L.t_rowptr = take(4u * (N + 1));
-    L.t_ldst = take(4u * Lk);
-    L.t_lrev = take(4u * E);
-    L.t_acctx = take(8u * N);
-    L.t_fsrc = take(4u * F);
-    L.t_fdst = take(4u * F);
-    L.t_fmean = take(8u * F);
     L.table_bytes = (uint32_t)(N * N);
-    L.topo_bytes = o;
-    topo.assign(o, 0);
-    memcpy(&topo[L.t_rowptr], T->row_ptr, 4u * (N + 1));
-    memcpy(&topo[L.t_ldst], ldst.data(), 4u * Lk);
-    memcpy(&topo[L.t_lrev], T->link_rev, 4u * E);
-    memcpy(&topo[L.t_acctx], acctx.data(), 8u * N);
-    memcpy(&topo[L.t_fsrc], T->flow_src, 4u * F);
-    memcpy(&topo[L.t_fdst], T->flow_dst, 4u * F);
-    std::vector<double> fmean(F);
+    L.topo_bytes = (uint32_t)sizeof(TopoImage);
+    if (Lk > 256 || E > 256 || F > 512) return set_err(PRISMA_ERR_CONFIG, "topology image limits exceeded");
+    topo.assign(sizeof(TopoImage), 0);
+    TopoImage& TI = *(TopoImage*)topo.data();
+    memcpy(TI.rowptr, T->row_ptr, 4u * (N + 1));
+    memcpy(TI.ldst, ldst.data(), 4u * Lk);
+    memcpy(TI.lrev, T->link_rev, 4u * E);
+    memcpy(TI.acctx, acctx.data(), 8u * N);
+    memcpy(TI.fsrc, T->flow_src, 4u * F);
+    memcpy(TI.fdst, T->flow_dst, 4u * F);
     for (int f = 0; f < F; ++f)                      // poisson-application.cc:280-283
-        fmean[f] = (double)(P->packet_size * 8u) / (double)T->flow_rate_bps[f];
-    memcpy(&topo[L.t_fmean], fmean.data(), 8u * F);
+        TI.fmean[f] = (double)(P->packet_size * 8u) / (double)T->flow_rate_bps[f];
 
     // state image: LDS part (staged into LDS) then register part (staged into VGPRs)
     int fs = 1, ls = 1;
@@ -1349,6 +1417,8 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.s_hdr = take(sizeof(Hdr));
     L.s_cnt = take(sizeof(prisma_counters_t));
     L.s_obs = take(4u * L.W);
+    if (L.s_hdr != kOffHdr || L.s_cnt != kOffCnt || L.s_obs != kOffObs)
+        return set_err(PRISMA_ERR_CONFIG, "internal: LDS header offsets");
     L.s_wt = take(4u * Lk * L.WCAP);
     L.s_wseq = take(4u * Lk * L.WCAP);
     L.s_ring = take(4u * tot);

@@ -11,7 +11,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "prisma_amd", "_ablate", "libprisma_amd_timing.so")
-NAMES = ["select", "arrive", "decision", "complete", "flow", "ping_round", "-", "-"]
+NAMES = ["select", "arrive", "decision", "complete", "flow", "ping_round", "dec:send", "dec:record"]
 
 if sys.argv[1] == "build":
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
@@ -46,7 +46,7 @@ lib.prisma_debug_timing(buf)
 hops = int(eng.counters()["hops_total"].sum()) - h0
 tot = sum(buf[i] for i in range(8))
 print(f"{topo_name} R={R}: cycles/hop/wave = {tot / max(1, hops):.0f}")
-for i in range(6):
-    n = buf[8 + i]
-    if n:
+for i in range(8):
+    n = buf[8 + i] if i < 6 else buf[8 + 2]
+    if n and buf[i]:
         print(f"  {NAMES[i]:11s} n/hop={n / hops:.3f}  cyc/call={buf[i] / n:8.0f}  share={buf[i] / tot:.3f}")
