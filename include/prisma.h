@@ -206,12 +206,18 @@ int prisma_reset(prisma_env_t* env, uint32_t episode, void* stream);
  * next pending decision.  obs_out: device int32 [n_replicas][obs_width];
  * mask_out: device uint8 [n_replicas] (1 = a decision is pending, 0 =
  * episode over); node_out: device int32 [n_replicas], the node deciding
- * (-1 if none).  Any output may be NULL. */
+ * (-1 if none).  Any output may be NULL.  A launch never crosses an episode
+ * boundary: a replica whose episode ends reports mask 0, and with
+ * params.auto_reset it starts its next episode before the call returns (on
+ * `stream`), so its next step continues there. */
 int prisma_step(prisma_env_t* env, const int32_t* actions, int32_t* obs_out,
                 uint8_t* mask_out, int32_t* node_out, void* stream);
 
 /* Fused policy: advance every replica by up to max_hops hops, deciding
- * in-kernel with `table` (device uint8 [n_nodes][n_nodes] action table). */
+ * in-kernel with `table` (device uint8 [n_nodes][n_nodes] action table).
+ * A replica stops early at the end of its episode; with params.auto_reset
+ * it starts the next episode before the call returns (one launch never
+ * crosses an episode boundary). */
 int prisma_run(prisma_env_t* env, int32_t policy, const uint8_t* table,
                int32_t max_hops, void* stream);
 

@@ -121,83 +121,16 @@ struct LA {
     }
 };
 
-// Per-episode counters updated in the event loop live in a register pair
-// (cv_lo, cv_hi): lane k holds counter slot k as 64 bits.  An update is a
-// full-wave add + select (no LDS read-modify-write to wait on); the slots are
-// moved from / to the prisma_counters_t image in LDS at launch entry / exit.
-enum CSlot : uint32_t {
-    C_EVENTS = 0, C_HOPS, C_DECISIONS, C_HOPDEG, C_REWARD, C_OV_INJ, C_OV_ARR, C_OV_LOST, C_BYTES_DATA,
-    C_BYTES_SIG, C_COST, C_E2E, C_COST_N, C_E2E_N, C_CTRL_DROP, C_NSLOTS
-};
-// byte offset and width (8: 64-bit) of each slot in prisma_counters_t
-__device__ __forceinline__ void cslot_field(uint32_t k, uint32_t& off, bool& wide) {
-    switch (k) {
-    case C_EVENTS: off = offsetof(prisma_counters_t, events); wide = true; break;
-    case C_HOPS: off = offsetof(prisma_counters_t, hops); wide = true; break;
-    case C_DECISIONS: off = offsetof(prisma_counters_t, decisions); wide = true; break;
-    case C_HOPDEG: off = offsetof(prisma_counters_t, hop_deg_sum); wide = true; break;
-    case C_REWARD: off = offsetof(prisma_counters_t, reward_sum); wide = true; break;
-    case C_OV_INJ: off = offsetof(prisma_counters_t, ov_injected); wide = false; break;
-    case C_OV_ARR: off = offsetof(prisma_counters_t, ov_arrived); wide = false; break;
-    case C_OV_LOST: off = offsetof(prisma_counters_t, ov_lost); wide = false; break;
-    case C_BYTES_DATA: off = offsetof(prisma_counters_t, bytes_data); wide = false; break;
-    case C_BYTES_SIG: off = offsetof(prisma_counters_t, bytes_signaling); wide = false; break;
-    case C_COST: off = offsetof(prisma_counters_t, cost_sum); wide = false; break;
-    case C_E2E: off = offsetof(prisma_counters_t, e2e_sum); wide = false; break;
-    case C_COST_N: off = offsetof(prisma_counters_t, cost_n); wide = false; break;
-    case C_E2E_N: off = offsetof(prisma_counters_t, e2e_n); wide = false; break;
-    default: off = offsetof(prisma_counters_t, ctrl_dropped); wide = false; break;
-    }
+// Per-episode counters live in the LDS image and are bumped by lane 0 with
+// no-return LDS atomics (ds_add_u32/u64/f32/f64): fire-and-forget, in order
+// per wave, and bit-identical to sequential IEEE adds on gfx950 (checked by
+// scripts/ubench/lds_fadd.hip) -- no read-modify-write to wait on, no VGPRs.
+template <class T>
+__device__ __forceinline__ void lds_add(T* p, T v) {
+    __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-
-// lane id the compiler cannot hoist comparisons of out of the event loop
-// (15 hoisted lane masks would cost 30 SGPRs)
-__device__ __forceinline__ uint32_t fresh_lane() {
-    uint32_t l = threadIdx.x;
-    asm volatile("" : "+v"(l));
-    return l;
-}
-
-struct CntV {
-    uint32_t lo, hi;
-    template <uint32_t K> __device__ __forceinline__ void add_u64(uint64_t v) {
-        const uint64_t n = (((uint64_t)hi << 32) | lo) + v;
-        const bool me = fresh_lane() == K;
-        lo = me ? (uint32_t)n : lo;
-        hi = me ? (uint32_t)(n >> 32) : hi;
-    }
-    template <uint32_t K> __device__ __forceinline__ void add_u32(uint32_t v) {
-        lo = (fresh_lane() == K) ? lo + v : lo;
-    }
-    template <uint32_t K> __device__ __forceinline__ void add_f32(float v) {
-        lo = (fresh_lane() == K) ? __float_as_uint(__uint_as_float(lo) + v) : lo;
-    }
-    template <uint32_t K> __device__ __forceinline__ void add_f64(double v) {
-        const uint64_t n = __double_as_longlong(__longlong_as_double((long long)(((uint64_t)hi << 32) | lo)) + v);
-        const bool me = fresh_lane() == K;
-        lo = me ? (uint32_t)n : lo;
-        hi = me ? (uint32_t)(n >> 32) : hi;
-    }
-    __device__ __forceinline__ void load(const prisma_counters_t* c, uint32_t lane) {
-        lo = 0; hi = 0;
-        if (lane < C_NSLOTS) {
-            uint32_t off; bool wide;
-            cslot_field(lane, off, wide);
-            const uint32_t* w = (const uint32_t*)((const unsigned char*)c + off);
-            lo = w[0];
-            hi = wide ? w[1] : 0u;
-        }
-    }
-    __device__ __forceinline__ void store(prisma_counters_t* c, uint32_t lane) const {
-        if (lane < C_NSLOTS) {
-            uint32_t off; bool wide;
-            cslot_field(lane, off, wide);
-            uint32_t* w = (uint32_t*)((unsigned char*)c + off);
-            w[0] = lo;
-            if (wide) w[1] = hi;
-        }
-    }
-};
+#define CNT_ADD(S_, field_, v_) \
+    do { if ((S_).lane == 0) lds_add(&(S_).c->field_, (decltype((S_).c->field_))(v_)); } while (0)
 
 // register-resident replica state (image order: the fields below, each a
 // [64*S] u32 array)
@@ -215,7 +148,6 @@ struct Regs {
     LA<LS> pav_lo, pav_hi;                       // ping window mean (double), refreshed per ping-back
     LA<LS> nd_lo, nd_hi, hd_lo, hd_hi;           // send time (s) of ping ack+1 and of the first hole
     static constexpr int NF = 4, NL = 20;
-    CntV cv;                                     // episode counters (not part of the register image)
 };
 
 template <int FS, int LS>
@@ -376,7 +308,6 @@ __device__ inline void hot_load(const Sim& S, Hot& H) {
 
 template <int FS, int LS>
 __device__ inline void hot_store(Sim& S, const Regs<FS, LS>& R, const Hot& H) {
-    R.cv.store(S.c, (uint32_t)S.lane);
     if (S.lane == 0) {
         Hdr& h = *S.h;
         h.now = H.now; h.ping_t = H.ping_t; h.ping_seq = H.ping_seq; h.seq = H.seq; h.uid = H.uid;
@@ -614,18 +545,18 @@ __device__ __forceinline__ void receive_counters(const Sim& S, Regs<FS, LS>& R, 
     const LV& L = S.lv;
     if (arrived) {
         // valable, nextHop == finalDest on identity overlays
-        R.cv.template add_u32<C_OV_ARR>(1u);
+        CNT_ADD(S, ov_arrived, 1u);
         const float cost = (float)(ns_to_sec(H.now) - (double)start);
-        R.cv.template add_f32<C_COST>(cost);
-        R.cv.template add_u32<C_COST_N>(1u);
-        R.cv.template add_f32<C_E2E>(cost);
-        R.cv.template add_u32<C_E2E_N>(1u);
+        CNT_ADD(S, cost_sum, cost);
+        CNT_ADD(S, cost_n, 1u);
+        CNT_ADD(S, e2e_sum, cost);
+        CNT_ADD(S, e2e_n, 1u);
     }
     // pings are always addressed to the node that receives them
-    if (!ent_is_data(x)) R.cv.template add_u32<C_BYTES_SIG>(L.ping_size() - 2u);
+    if (!ent_is_data(x)) CNT_ADD(S, bytes_signaling, L.ping_size() - 2u);
     if (ent_type(x) == T_FRESH) {
-        R.cv.template add_u32<C_OV_INJ>(1u);
-        R.cv.template add_u32<C_BYTES_DATA>(L.data_size() - 2u);
+        CNT_ADD(S, ov_injected, 1u);
+        CNT_ADD(S, bytes_data, L.data_size() - 2u);
     }
 }
 
@@ -645,17 +576,17 @@ __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Ho
     uint32_t status;
     if (action >= 0 && action < deg) {
         uint32_t l = (uint32_t)(r0 + action);
-        R.cv.template add_u64<C_HOPS>(1u);
-        R.cv.template add_u64<C_HOPDEG>((uint64_t)deg);
+        CNT_ADD(S, hops, 1u);
+        CNT_ADD(S, hop_deg_sum, (uint64_t)deg);
         const uint32_t fwd = (PRISMA_ABLATE & 1) ? (T_RELAY | (dst << 2) | (start << 10)) : r_make(d);
         if (link_send(S, R, H, l, fwd)) {                         // lastHop = v, previous decision = d
             status = PRISMA_ST_ENQUEUED;
         } else {
             status = PRISMA_ST_DROPPED;              // :655-664 + forwarder.py:214-244
-            R.cv.template add_u32<C_OV_LOST>(1u);
-            R.cv.template add_f32<C_COST>(L.loss_penalty_f());
-            R.cv.template add_u32<C_COST_N>(1u);
-            R.cv.template add_f64<C_REWARD>(L.loss_penalty());
+            CNT_ADD(S, ov_lost, 1u);
+            CNT_ADD(S, cost_sum, L.loss_penalty_f());
+            CNT_ADD(S, cost_n, 1u);
+            CNT_ADD(S, reward_sum, L.loss_penalty());
         }
     } else {
         status = PRISMA_ST_DISCARDED;
@@ -688,14 +619,14 @@ __device__ __forceinline__ void on_ping_round(const Sim& S, Regs<FS, LS>& R, Hot
     for (int u = 0; u < L.N(); ++u) {
         int r0 = S.T->rowptr[u], r1 = S.T->rowptr[u + 1];
         for (int l = r0; l < r1; ++l) {
-            if (!link_send(S, R, H, (uint32_t)l, p_make(T_PFWD, (uint32_t)(l - r0), k))) R.cv.template add_u32<C_CTRL_DROP>(1u);
+            if (!link_send(S, R, H, (uint32_t)l, p_make(T_PFWD, (uint32_t)(l - r0), k))) CNT_ADD(S, ctrl_dropped, 1u);
         }
         uint32_t s = H.seq++;                                    // re-arm of node u
         if (u == 0) first_rearm = s;
     }
     H.ping_rounds = k + 1;
     // one ns-3 event per node timer (the round is N consecutive events)
-    R.cv.template add_u64<C_EVENTS>((uint64_t)(L.N() - 1));
+    CNT_ADD(S, events, (uint64_t)(L.N() - 1));
     H.ev_launch += (uint32_t)(L.N() - 1);
     H.ping_t = H.now + L.ping_period();
     H.ping_seq = first_rearm;
@@ -796,10 +727,10 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             dst = (w_prev >> 8) & 255u;
             start = w_prev >> 16;
             reward = (double)py_micros(H.now) / 1e6 - (double)py_micros(t_prev) / 1e6;   // forwarder.py:360
-            R.cv.template add_f64<C_REWARD>(reward);
+            CNT_ADD(S, reward_sum, reward);
         }
         const uint32_t o = (S.lane == 0) ? dst : obs_links;
-        R.cv.template add_u64<C_DECISIONS>(1u);
+        CNT_ADD(S, decisions, 1u);
         if (dst == v) {                                             // getGameOver
             write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_DESTINATION, o);
             receive_counters(S, R, H, x, true, start);
@@ -815,7 +746,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     if (type == T_PFWD) {                                           // ping-forward-packet-manager.cc:94-156
         float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
         if (S.lane == 0) S.pbd[l * L.PBK() + (rnd & (L.PBK() - 1))] = delay;
-        if (!link_send(S, R, H, (uint32_t)S.T->lrev[l], p_make(T_PBACK, tun, rnd))) R.cv.template add_u32<C_CTRL_DROP>(1u);
+        if (!link_send(S, R, H, (uint32_t)S.T->lrev[l], p_make(T_PBACK, tun, rnd))) CNT_ADD(S, ctrl_dropped, 1u);
     } else {                                                        // ping-back-packet-manager.cc:120-144
         const uint32_t lt = (uint32_t)S.T->rowptr[v] + tun;
         const float delay = __uint_as_float(u_ld32((const uint32_t*)S.pbd + lt * L.PBK() + (rnd & (L.PBK() - 1))));
@@ -878,8 +809,6 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
     __syncthreads();
     uint4* st4 = (uint4*)S.base;
     for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes() / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
-    R.cv.lo = 0;
-    R.cv.hi = 0;
 #pragma unroll
     for (int j = 0; j < FS; ++j) {
         uint32_t f = (uint32_t)lane + 64u * j;
@@ -1080,19 +1009,35 @@ __device__ __forceinline__ void publish_counters(const Sim& S, const KParams& P,
     if (lane < (int)(sizeof(prisma_counters_t) / 4)) dst[lane] = src[lane];
 }
 
+// mode 0: (re)build every replica at episode P.episode.
+// mode 3 (auto-reset, launched after each step when auto_reset is set): a
+// replica whose episode ended (and did not fail) starts episode + 1, keeping
+// its decision-log position and running totals.  The event loop itself never
+// resets, so a launch never crosses an episode boundary.
 template <int FS, int LS>
 __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
     CLayout& LC = *(CLayout*)P.lay;
+    const unsigned char* img = P.state + (size_t)r * LC.state_bytes;
+    const Hdr* gh = (const Hdr*)(img + kOffHdr);
+    uint32_t episode = P.episode;
+    Hot H;
+    memset(&H, 0, sizeof(H));
+    const bool keep = (P.mode == 3);
+    if (keep) {
+        if (!rfl(gh->over) || rfl(gh->error)) return;           // replica still running (or failed)
+        episode = rfl(gh->episode) + 1u;
+        H.dec = rfl(gh->dec_count);
+        if (lane < (int)(sizeof(Hdr) / 4)) ((uint32_t*)(lds + kOffHdr))[lane] = ((const uint32_t*)gh)[lane];
+        __syncthreads();
+    }
     LV lv;
     lv.load(P.lay, lane);
     Sim S;
     sim_bind(S, lv, lds, P.topo, P.log + (size_t)r * LC.log_cap * LC.rec_bytes, LC.replica_base + (uint32_t)r, lane);
     Regs<FS, LS> R;
-    Hot H;
-    memset(&H, 0, sizeof(H));
-    init_replica(S, R, H, P.episode, false);
+    init_replica(S, R, H, episode, keep);
     hot_store(S, R, H);
     __syncthreads();
     publish_counters(S, P, r, lane);
@@ -1125,7 +1070,6 @@ prisma_step_kernel_t(KParams P) {
     const uint32_t NN = (uint32_t)L.N();
     Hot H;
     hot_load(S, H);
-    R.cv.load(S.c, (uint32_t)lane);
 
     H.stop = 0;
     H.hops_launch = 0;
@@ -1142,7 +1086,6 @@ prisma_step_kernel_t(KParams P) {
     }
     if (H.over || (table_mode && H.hops_launch >= max_hops)) H.stop = 1;
 
-    uint32_t resets = 0;
     // Drain the stage-in loads here: otherwise the waitcnt pass keeps them
     // "possibly pending" at the loop header and emits vmcnt waits there that,
     // on every later iteration, also wait for the previous event's record
@@ -1165,17 +1108,12 @@ prisma_step_kernel_t(KParams P) {
 #endif
         select_event(R, H, lane, bt, bc);
         if (bt >= L.t_end()) {                           // Simulator::Stop(simTime) (sim.cc:703)
-            if (L.auto_reset() && resets < 64u) {        // bounded: an empty scenario cannot spin forever
-                ++resets;
-                init_replica(S, R, H, H.episode + 1u, true);
-                continue;
-            }
             H.over = 1;
             H.stop = 1;
             break;
         }
         H.now = bt;
-        R.cv.template add_u64<C_EVENTS>(1u);
+        CNT_ADD(S, events, 1u);
         H.ev_launch++;
         const uint32_t kind = bc >> 28, id = bc & 0x0fffffffu;
         TM_MARK(0);
@@ -1511,6 +1449,14 @@ static int launch(prisma_env_t* e, const void* kern, KParams P, void* stream) {
     return PRISMA_OK;
 }
 
+// with auto_reset, replicas whose episode ended in the last launch start the next one
+static int auto_reset(prisma_env_t* e, void* stream) {
+    if (!e->lay.auto_reset) return PRISMA_OK;
+    KParams P = base_params(e);
+    P.mode = 3;
+    return launch(e, e->k_reset, P, stream);
+}
+
 extern "C" int prisma_reset(prisma_env_t* e, uint32_t episode, void* stream) {
     if (!e) return set_err(PRISMA_ERR_ARG, "null env");
     KParams P = base_params(e);
@@ -1532,7 +1478,8 @@ extern "C" int prisma_step(prisma_env_t* e, const int32_t* actions, int32_t* obs
     P.mask_out = mask_out;
     P.node_out = node_out;
     P.max_hops = 0x7fffffff;
-    return launch(e, e->k_step, P, stream);
+    int rc = launch(e, e->k_step, P, stream);
+    return rc ? rc : auto_reset(e, stream);
 }
 
 extern "C" int prisma_run(prisma_env_t* e, int32_t policy, const uint8_t* table, int32_t max_hops, void* stream) {
@@ -1544,7 +1491,8 @@ extern "C" int prisma_run(prisma_env_t* e, int32_t policy, const uint8_t* table,
     P.mode = 2;
     P.table = table;
     P.max_hops = max_hops;
-    return launch(e, e->k_step, P, stream);
+    int rc = launch(e, e->k_step, P, stream);
+    return rc ? rc : auto_reset(e, stream);
 }
 
 extern "C" int prisma_read_counters(prisma_env_t* e, prisma_counters_t* host_out, void* stream) {

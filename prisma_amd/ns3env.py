@@ -1,0 +1,224 @@
+"""Per-node ``Ns3Env`` drop-in over one GPU replica (the reference's gym surface).
+
+The reference runs one ns-3 process and, per overlay node, one
+``ns3env.Ns3Env(port=basePort+index, stepTime, startSim, simSeed, simArgs,
+debug)`` client (forwarder.py:47) that a Forwarder thread drives with
+``reset()`` / ``step(action)`` (forwarder.py:291-332; ns3env.py:378-440):
+
+* the constructor blocks until the simulator first notifies this node, and
+  ``reset()`` returns that observation;
+* ``step(action)`` applies the action to the packet this node was last shown,
+  then blocks until the simulator notifies this node again and returns
+  ``(obs, reward, done, info)``: obs = ``[dst, v_0..v_{deg-1}]``
+  (data-packet-manager.cc:171-206), reward = ``getReward()`` = 1,
+  done = packet at its destination (``getGameOver``, :219-227), info = the
+  22-token string of ``DataPacketManager::getInfo`` (packet-manager.cc:119-176,
+  data-packet-manager.cc:230-248) that ``Forwarder.treat_info`` parses;
+* at simulation end ``connected`` turns False (ns3env.py:211-213).
+
+Here the simulator is ``PrismaSession``: one replica of the HIP engine in
+external-action mode.  At most one decision is pending at a time, exactly as
+ns-3 blocks on each Notify; ``PrismaSession.apply`` hands the action to the
+engine, which runs on the GPU to the next data notification (any node).  The
+info string is rendered from the engine's decision record and counters.
+
+This is the slow, one-decision-per-launch compatibility path for unmodified
+agents; batched training/evaluation uses ``VecRoutingEnv`` (prisma_amd.env).
+"""
+from __future__ import annotations
+
+import threading
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from .config import engine_params
+from .engine import PrismaEngine
+from .env import Box, Discrete
+from .records import ST_DROPPED, ST_PENDING
+from .topology import Topology
+
+_SESSIONS: List["PrismaSession"] = []
+
+
+def _f(x: float) -> str:
+    return "%f" % x
+
+
+class PrismaSession:
+    """One simulated network (one engine replica) shared by the per-node envs."""
+
+    def __init__(self, topology: str = "abilene", tm_index: int = 0, load_factor: float = 1.0,
+                 base_port: int = 6555, device: int = 0, replica: int = 0, topo: Optional[Topology] = None,
+                 **params):
+        self.topo = topo if topo is not None else Topology.example(topology, tm_index, load_factor)
+        self.params = engine_params(self.topo, replica_base=replica, **params)
+        self.engine = PrismaEngine(self.topo, self.params, 1, device)
+        self.base_port = int(base_port)
+        self.N = self.topo.n_nodes
+        self.deg = [int(d) for d in self.topo.degrees]
+        self.data_size = int(self.params["packet_size"]) + 30          # UDP 8 + IP 20 + PPP 2
+        self._cv = threading.Condition()
+        self._lost: Dict[int, List[int]] = {u: [] for u in range(self.N)}
+        self._src: Dict[int, int] = {}                                   # uid -> source node
+        self._pending = None                                             # (node, obs, done, info, dec)
+        self._over = False
+        self._closed = 0
+        self.log: List[tuple] = []                                       # (node, obs, done, info) per notify
+        self.engine.reset(0)
+        self._advance(None)
+        _SESSIONS.append(self)
+
+    # -- simulator side ------------------------------------------------------
+    def _advance(self, action: Optional[int]):
+        import torch
+        a = None if action is None else torch.tensor([int(action)], dtype=torch.int32, device=self.engine.torch_device)
+        prev = self._pending
+        obs, mask, node = self.engine.step(a)
+        cnt = self.engine.counters()[0]
+        if prev is not None:
+            # the applied decision is final now: a drop is reported to the deciding node's
+            # next data notification (dropPacket -> getInfo "Packet Lost=", data-packet-manager.cc:88-98)
+            rec = self.engine.records(0, prev[4], 1)[0]
+            if int(rec["status"]) == ST_DROPPED:
+                self._lost[int(rec["node"])].append(int(rec["uid"]))
+                self._src.pop(int(rec["uid"]), None)
+        if int(mask.cpu()[0]) == 0:
+            self._pending = None
+            self._over = True
+            return
+        d = int(cnt["dec_count"]) - 1
+        rec = self.engine.records(0, d, 1)[0]
+        assert int(rec["status"]) == ST_PENDING
+        v = int(node.cpu()[0])
+        W = 1 + self.deg[v]
+        ob = [int(x) for x in obs.cpu().numpy()[0][:W]]
+        done = False
+        self._pending = (v, ob, done, self._render_info(rec, cnt, v), d)
+        if int(rec["prev"]) < 0:
+            self._src[int(rec["uid"])] = v
+        self.log.append(self._pending[:4])
+
+    def _render_info(self, rec, cnt, v: int) -> str:
+        """DataPacketManager::getInfo for the notified data packet (22 tokens)."""
+        now = int(rec["t_ns"]) / 1e9
+        e2e_n, cost_n = int(cnt["e2e_n"]), int(cnt["cost_n"])
+        avg_e2e = np.float32(cnt["e2e_sum"]) / np.float32(e2e_n) if e2e_n else np.float32(0.0)
+        avg_cost = np.float32(cnt["cost_sum"]) / np.float32(cost_n) if cost_n else np.float32(0.0)
+        bd = int(cnt["bytes_data"])
+        sig = np.float32(int(cnt["bytes_signaling"])) / np.float32(bd) if bd else np.float32(0.0)
+        lost, inj, arr = int(cnt["ov_lost"]), int(cnt["ov_injected"]), int(cnt["ov_arrived"])
+        ul, ui, ua = int(cnt["un_lost"]), int(cnt["un_injected"]), int(cnt["un_arrived"])
+        lv = self._lost[v]
+        lost_ids = "".join("%u;" % u for u in reversed(lv))
+        lv.clear()
+        uid = int(rec["uid"])
+        src = self._src.get(uid, v)
+        return (f"End to End Delay={_f(now - float(int(rec['start_s'])))}, Packet Size={self.data_size}, "
+                f"Current sim time ={_f(now)}, Pkt ID ={uid}, packetType =0"
+                f", Avg End to End Delay ={_f(float(avg_e2e))}, Avg Cost ={_f(float(avg_cost))}, "
+                f"Avg Underlay End to End Delay ={_f(0.0)}, Avg Underlay Cost ={_f(0.0)}"
+                f", Packets dropped ={lost}, Packets delivered ={arr}, Packets injected ={inj},"
+                f"Packets Buffered ={inj - (arr + lost)}"
+                f", Packets dropped Underlay ={ul}, Packets delivered Underlay={ua}, Packets injected Underlay={ui},"
+                f"Packets Buffered Underlay={ui - (ua + ul)}"
+                f",Signaling overhead ={_f(float(sig))}, Packet Lost={lost_ids}"
+                f", Source={src}, Destination={int(rec['dst'])}, node={v}")
+
+    # -- single-threaded driver (tests, notebooks) -----------------------------
+    def pending(self):
+        """(node, obs, done, info) of the decision the simulator waits for, or None at the end."""
+        with self._cv:
+            return None if self._pending is None else self._pending[:4]
+
+    def apply(self, action: int):
+        """Apply an action to the pending decision and run to the next notification."""
+        with self._cv:
+            if self._pending is None:
+                raise RuntimeError("simulation over")
+            v = self._pending[0]
+            done = self._pending[1][0] == v
+            if done:
+                action = 0          # at the destination the action is ignored (sendPacket :256-260)
+            self._advance(action)
+            self._cv.notify_all()
+
+    def over(self) -> bool:
+        return self._over
+
+    def counters(self):
+        return self.engine.counters()[0]
+
+    def close(self):
+        with self._cv:
+            self._closed += 1
+            if self._closed >= self.N or self._over:
+                self._over = True
+                self._cv.notify_all()
+
+    # -- per-node blocking view ------------------------------------------------
+    def _wait_for(self, node: int):
+        with self._cv:
+            while not self._over and (self._pending is None or self._pending[0] != node):
+                self._cv.wait()
+            return None if self._pending is None or self._pending[0] != node else self._pending[:4]
+
+    def _step_node(self, node: int, action: int):
+        with self._cv:
+            if self._pending is not None and self._pending[0] == node:
+                self._advance(action)
+                self._cv.notify_all()
+        return self._wait_for(node)
+
+
+def session_for_port(port: int) -> PrismaSession:
+    for s in reversed(_SESSIONS):
+        if s.base_port <= port < s.base_port + s.N:
+            return s
+    raise RuntimeError(f"no PrismaSession serves port {port}: create one with PrismaSession(base_port=...)")
+
+
+class _BridgeShim:
+    """The bits of Ns3ZmqBridge the Forwarder touches (send_close_command)."""
+
+    def __init__(self, env: "Ns3Env"):
+        self.env = env
+
+    def send_close_command(self):
+        self.env.session.close()
+        return True
+
+
+class Ns3Env:
+    """ns3env.Ns3Env signature; node = port - session.base_port."""
+
+    def __init__(self, stepTime=0, port=0, startSim=True, simSeed=0, simArgs={}, debug=False,
+                 session: Optional[PrismaSession] = None):
+        self.stepTime, self.port, self.startSim = stepTime, port, startSim
+        self.simSeed, self.simArgs, self.debug = simSeed, simArgs, debug
+        self.session = session if session is not None else session_for_port(int(port))
+        self.node = int(port) - self.session.base_port
+        deg = self.session.deg[self.node]
+        self.action_space = Discrete(deg)
+        self.observation_space = Box(0, 16260, (1 + deg,))
+        self.ns3ZmqBridge = _BridgeShim(self)
+        self.connected = True
+        self._state = self._to_state(self.session._wait_for(self.node))
+
+    def _to_state(self, st):
+        if st is None:
+            self.connected = False
+            prev = getattr(self, "_state", None)
+            return prev if prev is not None else ([-1], 1.0, True, "")
+        v, obs, _, info = st
+        return (list(obs), 1.0, obs[0] == v, info)
+
+    def reset(self):
+        return self._state[0]
+
+    def step(self, action):
+        self._state = self._to_state(self.session._step_node(self.node, int(action)))
+        return self._state
+
+    def close(self):
+        self.session.close()

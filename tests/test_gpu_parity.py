@@ -124,29 +124,37 @@ def test_episode_end_and_auto_reset(oracle_mod):
         assert cnt[r]["episode_over"] == 1
         assert_counters_equal(cnt[r], o.counters(), r)
     eng.close()
-    # with auto-reset, episode 1 equals a fresh oracle episode 1
+    # with auto-reset, the launch stops at the episode end, the replica starts
+    # episode 1 before run() returns, and episode 1 equals a fresh oracle episode 1
     params = dict(base, auto_reset=1)
     eng = PrismaEngine(topo, params, 2)
     eng.reset(0)
     t = torch.from_numpy(sp_next_hop_table(topo)).cuda()
-    eng.run(t, 6000)
+    eng.run(t, 10 ** 6)
+    cnt = eng.counters()
+    h0 = cnt["hops_total"].copy()
+    assert np.all(cnt["episode"] == 1) and np.all(cnt["episode_over"] == 0) and np.all(cnt["hops"] == 0)
+    eng.run(t, 2000)
     torch.cuda.synchronize()
     cnt = eng.counters()
     log = eng.log_tensor().cpu().numpy()
     for r in range(2):
-        assert cnt[r]["episode"] >= 1
         o0 = oracle_mod.OracleSim(topo, base, replica=r, episode=0)
         o0.run_table(sp_next_hop_table(topo), 10 ** 9)
         n0 = len(o0.records())
+        assert int(h0[r]) == int(o0.counters()["hops"])
         o1 = oracle_mod.OracleSim(topo, base, replica=r, episode=1)
-        o1.run_table(sp_next_hop_table(topo), 10 ** 9)
+        o1.run_table(sp_next_hop_table(topo), 2000)
         ref1 = o1.records()
-        n1 = min(len(ref1), int(cnt[r]["dec_count"]) - n0)
-        got = eng.records(r, n0, n1, log_host=log).copy()
+        assert int(cnt[r]["dec_count"]) - n0 == len(ref1)
+        got = eng.records(r, n0, len(ref1), log_host=log).copy()
         assert np.all(got["episode"] == 1)
         got["prev"] = np.where(got["prev"] >= 0, got["prev"] - n0, got["prev"])
-        assert got.tobytes() == ref1[:n1].tobytes()
-        assert int(cnt[r]["hops_total"]) == 6000
+        assert got.tobytes() == ref1.tobytes()
+        assert int(cnt[r]["hops_total"]) == int(h0[r]) + 2000
+        o1c = o1.counters()
+        o1c["dec_count"] += n0                      # the log position carries over episodes
+        assert_counters_equal(cnt[r], o1c, r)
     eng.close()
 
 
