@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PRISMA_ABI_VERSION 2
+#define PRISMA_ABI_VERSION 3
 
 /* status codes */
 #define PRISMA_OK              0
@@ -116,6 +116,10 @@ typedef struct prisma_params {
     uint32_t log_capacity;      /* records kept per replica (power of 2,
                                    >= 1024; must exceed the decisions made
                                    while one packet crosses one link)      */
+    uint32_t notify_dest;       /* prisma_step also stops at arrivals at the
+                                   destination (done=True notifications the
+                                   reference hands to the agent; the action
+                                   given for them is ignored)              */
 } prisma_params_t;
 
 /*

@@ -33,7 +33,7 @@ class OrConfig(C.Structure):
         ("packet_size", C.c_uint32), ("sim_time_s", C.c_double), ("ping_interval_s", C.c_float),
         ("ma_size", C.c_uint32), ("ping_as_obs", C.c_uint32), ("auto_reset", C.c_uint32),
         ("loss_penalty", C.c_double), ("seed", C.c_uint64), ("replica", C.c_uint32),
-        ("episode", C.c_uint32),
+        ("episode", C.c_uint32), ("notify_dest", C.c_uint32),
     ]
 
 
@@ -122,6 +122,7 @@ class OracleSim:
         cfg.seed = int(params["seed"])
         cfg.replica = int(replica)
         cfg.episode = int(episode)
+        cfg.notify_dest = int(params.get("notify_dest", 0))
         self._cfg = cfg
         self.W = topo.obs_width
         self.rec_dtype = record_dtype(self.W)

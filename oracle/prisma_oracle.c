@@ -187,7 +187,7 @@ struct or_sim {
     /* records */
     unsigned char* rec; int64_t rec_n, rec_cap; int rec_bytes;
     /* pending decision */
-    int pend; int pend_pkt, pend_node, pend_link; int64_t pend_rec;
+    int pend; int pend_pkt, pend_node, pend_link; int64_t pend_rec; int pend_dest;
     int over;
     /* trace */
     int trace_on; int64_t* tr; int64_t tr_n, tr_cap;
@@ -554,6 +554,13 @@ static void receive_counters(or_sim_t* s, const pkt_t* k, int v) {
 static void finish_data_decision(or_sim_t* s, int action) {
     int p = s->pend_pkt, v = s->pend_node;
     int64_t d = s->pend_rec;
+    if (s->pend_dest) {                 /* done=True notification: sendPacket does nothing (:256-260) */
+        receive_counters(s, &s->pk[p], v);
+        pkt_free(s, p);
+        s->pend = 0;
+        s->pend_dest = 0;
+        return;
+    }
     pkt_t orig = s->pk[p];
     int deg = s->c.row_ptr[v + 1] - s->c.row_ptr[v];
     rec_head_t* r = rec_at(s, d);
@@ -618,6 +625,10 @@ static int receive(or_sim_t* s, int di, int p) {
         s->cnt.decisions++;
         if (k->dst == v) {                                            /* getGameOver: done */
             r->status = ST_DEST;
+            if (s->c.notify_dest) {                                   /* the agent sees it (done=True) */
+                s->pend = 1; s->pend_dest = 1; s->pend_pkt = p; s->pend_node = v; s->pend_link = di; s->pend_rec = dn;
+                return 1;
+            }
             receive_counters(s, k, v);                                /* sendPacket does nothing */
             pkt_free(s, p);
             return 0;

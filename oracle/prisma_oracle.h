@@ -43,6 +43,8 @@ typedef struct or_config {
     uint64_t seed;
     uint32_t replica;           /* global replica id (Philox key word 1)   */
     uint32_t episode;
+    uint32_t notify_dest;       /* or_step also stops at destination
+                                   notifications (their action is ignored) */
 } or_config_t;
 
 typedef struct or_sim or_sim_t;

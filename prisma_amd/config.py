@@ -68,7 +68,7 @@ def engine_params(topo: Topology, *, sim_time_s: float = 60.0, seed: int = 100, 
                   ping_interval_s: float = 0.2, ma_size: int = 5, link_cap: int = 500000,
                   link_delay_ms: float = 1.0, max_buffer: int = 16260, packet_size: int = 512,
                   auto_reset: int = 0, log_capacity: int = 8192, replica_base: int = 0,
-                  loss_penalty: Optional[float] = None, train: int = 0) -> dict:
+                  loss_penalty: Optional[float] = None, train: int = 0, notify_dest: int = 0) -> dict:
     """prisma_params_t as a dict (shared by the engine binding and the oracle)."""
     if train:
         raise NotImplementedError("train=1 small-signalling echoes (SURVEY 8a A14) are not modelled; "
@@ -81,5 +81,5 @@ def engine_params(topo: Topology, *, sim_time_s: float = 60.0, seed: int = 100, 
         max_buffer_bytes=int(max_buffer), packet_size=int(packet_size), sim_time_s=float(sim_time_s),
         ping_interval_s=float(ping_interval_s), ma_size=int(ma_size), ping_as_obs=int(ping_as_obs),
         auto_reset=int(auto_reset), loss_penalty=float(lp), seed=int(seed),
-        replica_base=int(replica_base), log_capacity=int(log_capacity),
+        replica_base=int(replica_base), log_capacity=int(log_capacity), notify_dest=int(notify_dest),
     )

@@ -49,7 +49,7 @@ struct Hdr {                 // 128 bytes at state offset 0
     uint32_t pend_link;
     uint32_t pend_node;
     uint32_t pend_dec;
-    uint32_t pend_ent[4];
+    uint32_t pend_ent[4];    // entry, dst, start second, 1 = destination notification
     uint32_t ping_rounds;
     uint32_t episode;
     uint32_t over;
@@ -94,7 +94,7 @@ struct Layout {
     // scenario constants
     int64_t  t_end, ping_period;
     uint32_t data_size, ping_size;
-    uint32_t ma, ping_as_obs, auto_reset;
+    uint32_t ma, ping_as_obs, auto_reset, notify_dest;
     uint32_t seed_lo, replica_base;
     uint32_t log_cap, rec_bytes;
     double   loss_penalty;

@@ -234,6 +234,7 @@ struct LV {
     __device__ __forceinline__ uint32_t ma() const { return (uint32_t)u(offsetof(Layout, ma) / 4); }
     __device__ __forceinline__ uint32_t ping_as_obs() const { return (uint32_t)u(offsetof(Layout, ping_as_obs) / 4); }
     __device__ __forceinline__ uint32_t auto_reset() const { return (uint32_t)u(offsetof(Layout, auto_reset) / 4); }
+    __device__ __forceinline__ uint32_t notify_dest() const { return (uint32_t)u(offsetof(Layout, notify_dest) / 4); }
     __device__ __forceinline__ uint32_t seed_lo() const { return (uint32_t)u(offsetof(Layout, seed_lo) / 4); }
     __device__ __forceinline__ uint32_t replica_base() const { return (uint32_t)u(offsetof(Layout, replica_base) / 4); }
     __device__ __forceinline__ uint32_t log_cap() const { return (uint32_t)u(offsetof(Layout, log_cap) / 4); }
@@ -602,12 +603,19 @@ __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Ho
 #endif
 }
 
+// returns 1 if a hop was executed (0 for a destination notification, whose
+// action is ignored: sendPacket at the destination does nothing, :256-260)
 template <int FS, int LS>
-__device__ __forceinline__ void finish_pending(const Sim& S, Regs<FS, LS>& R, Hot& H, int action) {
+__device__ __forceinline__ int finish_pending(const Sim& S, Regs<FS, LS>& R, Hot& H, int action) {
     const Hdr& h = *S.h;
+    H.pend = 0;
+    if (u_ld32(&h.pend_ent[3])) {
+        receive_counters(S, R, H, u_ld32(&h.pend_ent[0]), true, u_ld32(&h.pend_ent[2]));
+        return 0;
+    }
     apply_decision(S, R, H, u_ld32(&h.pend_ent[0]), 0u, 0u, 0u, u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action,
                    false, 0.0, 0, 0u);
-    H.pend = 0;
+    return 1;
 }
 
 // ---- handlers (uniform) ------------------------------------------------------
@@ -674,7 +682,7 @@ __device__ __forceinline__ void wire_pop(const Sim& S, Regs<FS, LS>& R, const Ho
 }
 
 struct Decision {
-    uint32_t x, dst, start, uid, v, d; double reward; int32_t prev; uint32_t obs;
+    uint32_t x, dst, start, uid, v, d; double reward; int32_t prev; uint32_t obs, dest;
 };
 
 // returns 1 if a data decision needs an action
@@ -731,8 +739,13 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
         }
         const uint32_t o = (S.lane == 0) ? dst : obs_links;
         CNT_ADD(S, decisions, 1u);
+        D.dest = 0;
         if (dst == v) {                                             // getGameOver
             write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_DESTINATION, o);
+            if (!fused && L.notify_dest()) {                        // the agent is notified (done=True)
+                D.x = x; D.dst = dst; D.start = start; D.v = v; D.d = d; D.obs = o; D.dest = 1;
+                return 1;
+            }
             receive_counters(S, R, H, x, true, start);
             return 0;
         }
@@ -1076,8 +1089,7 @@ prisma_step_kernel_t(KParams P) {
     if (H.pend && !H.over) {
         if (table_mode) {
             uint32_t pn = u_ld32(&S.h->pend_node), pd = u_ld32(&S.h->pend_ent[1]);
-            finish_pending(S, R, H, (int)rfl((uint32_t)S.table[pn * NN + pd]));
-            H.hops_launch++;
+            H.hops_launch += finish_pending(S, R, H, (int)rfl((uint32_t)S.table[pn * NN + pd]));
         } else if (P.actions) {
             finish_pending(S, R, H, (int)rfl((uint32_t)P.actions[r]));
         } else {
@@ -1133,7 +1145,7 @@ prisma_step_kernel_t(KParams P) {
                     if (lane == 0) {
                         Hdr& h = *S.h;
                         h.pend_link = id; h.pend_node = D.v; h.pend_dec = D.d;
-                        h.pend_ent[0] = D.x; h.pend_ent[1] = D.dst;
+                        h.pend_ent[0] = D.x; h.pend_ent[1] = D.dst; h.pend_ent[2] = D.start; h.pend_ent[3] = D.dest;
                     }
                     if (lane < L.W()) S.obs[lane] = D.obs;
                     H.pend = 1;
@@ -1374,6 +1386,7 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.ma = P->ma_size;
     L.ping_as_obs = P->ping_as_obs ? 1u : 0u;
     L.auto_reset = P->auto_reset ? 1u : 0u;
+    L.notify_dest = P->notify_dest ? 1u : 0u;
     L.seed_lo = (uint32_t)P->seed;
     L.replica_base = P->replica_base;
     L.log_cap = P->log_capacity;

@@ -35,7 +35,7 @@ import numpy as np
 from .config import engine_params
 from .engine import PrismaEngine
 from .env import Box, Discrete
-from .records import ST_DROPPED, ST_PENDING
+from .records import ST_DESTINATION, ST_DROPPED, ST_PENDING
 from .topology import Topology
 
 _SESSIONS: List["PrismaSession"] = []
@@ -45,6 +45,58 @@ def _f(x: float) -> str:
     return "%f" % x
 
 
+class InfoTracker:
+    """State behind the info string that is not in one record: the packets a
+    node lost since its last data notification (dropPacket ->
+    "Packet Lost=", data-packet-manager.cc:88-98) and each packet's source."""
+
+    def __init__(self, n_nodes: int, data_size: int):
+        self.lost: Dict[int, List[int]] = {u: [] for u in range(n_nodes)}
+        self.src: Dict[int, int] = {}
+        self.data_size = int(data_size)
+
+    def notified(self, rec):
+        """A data notification (record just written, status PENDING or DESTINATION)."""
+        if int(rec["prev"]) < 0:
+            self.src[int(rec["uid"])] = int(rec["node"])
+
+    def applied(self, rec):
+        """The decision of `rec` was applied (final status)."""
+        st = int(rec["status"])
+        if st == ST_DROPPED:
+            self.lost[int(rec["node"])].append(int(rec["uid"]))
+            self.src.pop(int(rec["uid"]), None)
+        elif st == ST_DESTINATION:
+            self.src.pop(int(rec["uid"]), None)
+
+    def render(self, rec, cnt) -> str:
+        """DataPacketManager::getInfo for the notified data packet (22 tokens)."""
+        v = int(rec["node"])
+        now = int(rec["t_ns"]) / 1e9
+        e2e_n, cost_n = int(cnt["e2e_n"]), int(cnt["cost_n"])
+        avg_e2e = np.float32(cnt["e2e_sum"]) / np.float32(e2e_n) if e2e_n else np.float32(0.0)
+        avg_cost = np.float32(cnt["cost_sum"]) / np.float32(cost_n) if cost_n else np.float32(0.0)
+        bd = int(cnt["bytes_data"])
+        sig = np.float32(int(cnt["bytes_signaling"])) / np.float32(bd) if bd else np.float32(0.0)
+        lost, inj, arr = int(cnt["ov_lost"]), int(cnt["ov_injected"]), int(cnt["ov_arrived"])
+        ul, ui, ua = int(cnt["un_lost"]), int(cnt["un_injected"]), int(cnt["un_arrived"])
+        lv = self.lost[v]
+        lost_ids = "".join("%u;" % u for u in reversed(lv))
+        lv.clear()
+        uid = int(rec["uid"])
+        src = self.src.get(uid, v)
+        return (f"End to End Delay={_f(now - float(int(rec['start_s'])))}, Packet Size={self.data_size}, "
+                f"Current sim time ={_f(now)}, Pkt ID ={uid}, packetType =0"
+                f", Avg End to End Delay ={_f(float(avg_e2e))}, Avg Cost ={_f(float(avg_cost))}, "
+                f"Avg Underlay End to End Delay ={_f(0.0)}, Avg Underlay Cost ={_f(0.0)}"
+                f", Packets dropped ={lost}, Packets delivered ={arr}, Packets injected ={inj},"
+                f"Packets Buffered ={inj - (arr + lost)}"
+                f", Packets dropped Underlay ={ul}, Packets delivered Underlay={ua}, Packets injected Underlay={ui},"
+                f"Packets Buffered Underlay={ui - (ua + ul)}"
+                f",Signaling overhead ={_f(float(sig))}, Packet Lost={lost_ids}"
+                f", Source={src}, Destination={int(rec['dst'])}, node={v}")
+
+
 class PrismaSession:
     """One simulated network (one engine replica) shared by the per-node envs."""
 
@@ -52,15 +104,14 @@ class PrismaSession:
                  base_port: int = 6555, device: int = 0, replica: int = 0, topo: Optional[Topology] = None,
                  **params):
         self.topo = topo if topo is not None else Topology.example(topology, tm_index, load_factor)
-        self.params = engine_params(self.topo, replica_base=replica, **params)
+        self.params = engine_params(self.topo, replica_base=replica, notify_dest=1, **params)
         self.engine = PrismaEngine(self.topo, self.params, 1, device)
         self.base_port = int(base_port)
         self.N = self.topo.n_nodes
         self.deg = [int(d) for d in self.topo.degrees]
         self.data_size = int(self.params["packet_size"]) + 30          # UDP 8 + IP 20 + PPP 2
         self._cv = threading.Condition()
-        self._lost: Dict[int, List[int]] = {u: [] for u in range(self.N)}
-        self._src: Dict[int, int] = {}                                   # uid -> source node
+        self.tracker = InfoTracker(self.N, self.data_size)
         self._pending = None                                             # (node, obs, done, info, dec)
         self._over = False
         self._closed = 0
@@ -77,53 +128,20 @@ class PrismaSession:
         obs, mask, node = self.engine.step(a)
         cnt = self.engine.counters()[0]
         if prev is not None:
-            # the applied decision is final now: a drop is reported to the deciding node's
-            # next data notification (dropPacket -> getInfo "Packet Lost=", data-packet-manager.cc:88-98)
-            rec = self.engine.records(0, prev[4], 1)[0]
-            if int(rec["status"]) == ST_DROPPED:
-                self._lost[int(rec["node"])].append(int(rec["uid"]))
-                self._src.pop(int(rec["uid"]), None)
+            self.tracker.applied(self.engine.records(0, prev[4], 1)[0])
         if int(mask.cpu()[0]) == 0:
             self._pending = None
             self._over = True
             return
         d = int(cnt["dec_count"]) - 1
         rec = self.engine.records(0, d, 1)[0]
-        assert int(rec["status"]) == ST_PENDING
+        assert int(rec["status"]) in (ST_PENDING, ST_DESTINATION)
         v = int(node.cpu()[0])
-        W = 1 + self.deg[v]
-        ob = [int(x) for x in obs.cpu().numpy()[0][:W]]
-        done = False
-        self._pending = (v, ob, done, self._render_info(rec, cnt, v), d)
-        if int(rec["prev"]) < 0:
-            self._src[int(rec["uid"])] = v
+        ob = [int(x) for x in obs.cpu().numpy()[0][:1 + self.deg[v]]]
+        self.tracker.notified(rec)
+        done = int(rec["status"]) == ST_DESTINATION
+        self._pending = (v, ob, done, self.tracker.render(rec, cnt), d)
         self.log.append(self._pending[:4])
-
-    def _render_info(self, rec, cnt, v: int) -> str:
-        """DataPacketManager::getInfo for the notified data packet (22 tokens)."""
-        now = int(rec["t_ns"]) / 1e9
-        e2e_n, cost_n = int(cnt["e2e_n"]), int(cnt["cost_n"])
-        avg_e2e = np.float32(cnt["e2e_sum"]) / np.float32(e2e_n) if e2e_n else np.float32(0.0)
-        avg_cost = np.float32(cnt["cost_sum"]) / np.float32(cost_n) if cost_n else np.float32(0.0)
-        bd = int(cnt["bytes_data"])
-        sig = np.float32(int(cnt["bytes_signaling"])) / np.float32(bd) if bd else np.float32(0.0)
-        lost, inj, arr = int(cnt["ov_lost"]), int(cnt["ov_injected"]), int(cnt["ov_arrived"])
-        ul, ui, ua = int(cnt["un_lost"]), int(cnt["un_injected"]), int(cnt["un_arrived"])
-        lv = self._lost[v]
-        lost_ids = "".join("%u;" % u for u in reversed(lv))
-        lv.clear()
-        uid = int(rec["uid"])
-        src = self._src.get(uid, v)
-        return (f"End to End Delay={_f(now - float(int(rec['start_s'])))}, Packet Size={self.data_size}, "
-                f"Current sim time ={_f(now)}, Pkt ID ={uid}, packetType =0"
-                f", Avg End to End Delay ={_f(float(avg_e2e))}, Avg Cost ={_f(float(avg_cost))}, "
-                f"Avg Underlay End to End Delay ={_f(0.0)}, Avg Underlay Cost ={_f(0.0)}"
-                f", Packets dropped ={lost}, Packets delivered ={arr}, Packets injected ={inj},"
-                f"Packets Buffered ={inj - (arr + lost)}"
-                f", Packets dropped Underlay ={ul}, Packets delivered Underlay={ua}, Packets injected Underlay={ui},"
-                f"Packets Buffered Underlay={ui - (ua + ul)}"
-                f",Signaling overhead ={_f(float(sig))}, Packet Lost={lost_ids}"
-                f", Source={src}, Destination={int(rec['dst'])}, node={v}")
 
     # -- single-threaded driver (tests, notebooks) -----------------------------
     def pending(self):
@@ -136,11 +154,7 @@ class PrismaSession:
         with self._cv:
             if self._pending is None:
                 raise RuntimeError("simulation over")
-            v = self._pending[0]
-            done = self._pending[1][0] == v
-            if done:
-                action = 0          # at the destination the action is ignored (sendPacket :256-260)
-            self._advance(action)
+            self._advance(action)            # at a destination the action is ignored (:256-260)
             self._cv.notify_all()
 
     def over(self) -> bool:
@@ -210,8 +224,8 @@ class Ns3Env:
             self.connected = False
             prev = getattr(self, "_state", None)
             return prev if prev is not None else ([-1], 1.0, True, "")
-        v, obs, _, info = st
-        return (list(obs), 1.0, obs[0] == v, info)
+        v, obs, done, info = st
+        return (list(obs), 1.0, bool(done), info)
 
     def reset(self):
         return self._state[0]

@@ -1,0 +1,130 @@
+"""Per-node Ns3Env compatibility surface (prisma_amd/ns3env.py).
+
+CPU: the info-string renderer + tracker, driven by the oracle in
+notify-destination mode, reproduces the oracle's own DataPacketManager::getInfo
+string at every notification (packet-manager.cc:119-176).
+GPU: PrismaSession (one engine replica) yields the same notification stream
+(node, obs, done, info) as the oracle, and per-node Ns3Env views driven by one
+thread per node (forwarder.py:291-332) see exactly that stream.
+"""
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+from prisma_amd.config import engine_params
+from prisma_amd.ns3env import InfoTracker
+from prisma_amd.topology import Topology, sp_next_hop_table
+
+
+def oracle_stream(oracle_mod, topo, params, policy, n):
+    """(node, obs, done, info) of the first n notifications of the oracle."""
+    o = oracle_mod.OracleSim(topo, params)
+    out = []
+    obs = o.step(-1)
+    while obs is not None and len(out) < n:
+        rec = o.records()[-1]
+        v = int(rec["node"])
+        W = 1 + int(topo.degrees[v])
+        done = int(rec["status"]) == 3
+        out.append((v, [int(x) for x in obs[:W]], done, o.last_info()))
+        obs = o.step(policy(v, obs))
+    return o, out
+
+
+def sp_policy(topo):
+    table = sp_next_hop_table(topo)
+    return lambda v, obs: 0 if obs[0] == v else int(table[v, obs[0]])
+
+
+def test_info_renderer_matches_oracle(oracle_mod):
+    topo = Topology.example("abilene", 0, 2.0)               # load 2.0: drops fill "Packet Lost="
+    params = engine_params(topo, sim_time_s=3.0, ping_as_obs=1, notify_dest=1)
+    o = oracle_mod.OracleSim(topo, params)
+    tr = InfoTracker(topo.n_nodes, 542)
+    table = sp_next_hop_table(topo)
+    obs = o.step(-1)
+    n, lost_seen, dest_seen = 0, 0, 0
+    while obs is not None and n < 4000:
+        recs = o.records()
+        rec = recs[-1]
+        tr.notified(rec)
+        info = tr.render(rec, o.counters())
+        assert info == o.last_info(), (n, info, o.last_info())
+        lost_seen += "Packet Lost=," not in info
+        v = int(rec["node"])
+        dest_seen += int(rec["status"]) == 3
+        d = len(recs) - 1
+        obs = o.step(0 if obs[0] == v else int(table[v, obs[0]]))
+        tr.applied(o.records(d, 1)[0])
+        n += 1
+    assert lost_seen > 0 and dest_seen > 0
+
+
+def test_notify_dest_does_not_change_the_trajectory(oracle_mod):
+    topo = Topology.example("abilene")
+    base = engine_params(topo, sim_time_s=3.0, ping_as_obs=0)
+    a = oracle_mod.OracleSim(topo, base)
+    a.run_table(sp_next_hop_table(topo), 10 ** 9)
+    o, stream = oracle_stream(oracle_mod, topo, dict(base, notify_dest=1), sp_policy(topo), 10 ** 9)
+    assert a.records().tobytes() == o.records().tobytes()
+    ca, co = a.counters(), o.counters()
+    assert ca.tobytes() == co.tobytes()
+    assert any(s[2] for s in stream)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")
+def test_session_stream_matches_oracle(oracle_mod):
+    from prisma_amd.ns3env import PrismaSession
+    topo = Topology.example("abilene", 0, 2.0)
+    kw = dict(sim_time_s=2.0, ping_as_obs=1)
+    pol = sp_policy(topo)
+    _, ref = oracle_stream(oracle_mod, topo, engine_params(topo, notify_dest=1, **kw), pol, 1500)
+    s = PrismaSession(topo=topo, base_port=7000, **kw)
+    got = []
+    while s.pending() is not None and len(got) < len(ref):
+        v, obs, done, info = s.pending()
+        got.append((v, obs, done, info))
+        s.apply(pol(v, obs))
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert g == r, (i, g, r)
+    assert len(got) == len(ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")
+def test_threaded_per_node_envs(oracle_mod):
+    """One Forwarder-like thread per node over Ns3Env(port=base+node)."""
+    from prisma_amd.ns3env import Ns3Env, PrismaSession
+    topo = Topology.example("abilene")
+    kw = dict(sim_time_s=1.5, ping_as_obs=1)
+    pol = sp_policy(topo)
+    s = PrismaSession(topo=topo, base_port=7100, **kw)
+    seen = {u: [] for u in range(topo.n_nodes)}
+    errors = []
+
+    def forwarder(u):
+        try:
+            env = Ns3Env(port=7100 + u, stepTime=0, startSim=0, simSeed=100)
+            obs = env.reset()
+            while env.connected:
+                seen[u].append(list(obs))
+                obs, _, done, info = env.step(pol(u, obs))
+            env.ns3ZmqBridge.send_close_command()
+        except Exception as e:                       # pragma: no cover - surfaced below
+            errors.append(e)
+
+    ths = [threading.Thread(target=forwarder, args=(u,)) for u in range(topo.n_nodes)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=600)
+    assert not errors and not any(t.is_alive() for t in ths)
+    o, ref = oracle_stream(oracle_mod, topo, engine_params(topo, notify_dest=1, **kw), pol, 10 ** 9)
+    for u in range(topo.n_nodes):
+        assert seen[u] == [obs for (v, obs, _, _) in ref if v == u], u
+    got, want = s.counters(), o.counters()
+    for k in ("hops", "decisions", "ov_injected", "ov_arrived", "ov_lost", "reward_sum", "cost_sum", "dec_count"):
+        assert got[k] == want[k], k
