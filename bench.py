@@ -45,7 +45,7 @@ def parse():
     p.add_argument("--load-factor", type=float, default=1.0)
     p.add_argument("--ping-as-obs", type=int, default=1)
     p.add_argument("--cpu-baseline", type=int, default=1)
-    p.add_argument("--cpu-hops", type=int, default=1000000, help="oracle hops per sampled replica")
+    p.add_argument("--cpu-hops", type=int, default=8000000, help="oracle hops per host thread (cpu_baseline)")
     return p.parse_args()
 
 
@@ -54,17 +54,25 @@ def algorithmic_bytes(hops: int, deg_sum: int) -> int:
     return 85 * hops + 12 * deg_sum
 
 
-def cpu_baseline(topo, params, table, hops_per_replica: int):
-    """The C oracle (oracle/, kind 'port') on host threads, one replica per thread."""
+def cpu_baseline(topo, params, table, hops_per_thread: int):
+    """The C oracle (oracle/, kind 'port') on host threads: each thread runs one
+    replica's episodes back to back (as auto-reset does) until it executed
+    `hops_per_thread` hops, on the same scenario and DQ-routing table."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
     cores = max(1, min(16, os.cpu_count() or 1))
-    sims = [O.OracleSim(topo, params, replica=100000 + i) for i in range(cores)]
     done = [0] * cores
+    episodes = [0] * cores
 
     def work(i):
-        done[i] = sims[i].run_table(table, hops_per_replica)   # ctypes releases the GIL
+        ep = 0
+        while done[i] < hops_per_thread:
+            sim = O.OracleSim(topo, params, replica=100000 + i, episode=ep)
+            done[i] += sim.run_table(table, hops_per_thread - done[i])   # ctypes releases the GIL
+            sim.close()
+            ep += 1
+        episodes[i] = ep
 
     ths = [threading.Thread(target=work, args=(i,)) for i in range(cores)]
     t0 = time.perf_counter()
@@ -73,12 +81,11 @@ def cpu_baseline(topo, params, table, hops_per_replica: int):
     for t in ths:
         t.join()
     dt = time.perf_counter() - t0
-    for s in sims:
-        s.close()
     hops = int(sum(done))
     return {"value": hops / dt, "unit": "hops/s", "cores": cores, "kind": "port",
-            "sample": f"{cores} Abilene replicas x {hops_per_replica} hops (same params and DQ-routing table), "
-                      f"one replica per host thread, {dt:.2f} s wall; ns-3 reference path not runnable (SURVEY 8c)"}
+            "sample": f"{cores} host threads x {hops_per_thread} hops ({sum(episodes)} Abilene episodes of "
+                      f"{params['sim_time_s']:g} s, same params and DQ-routing table), {hops} hops in {dt:.1f} s wall; "
+                      f"the ns-3 reference path is not runnable here (SURVEY 8c)"}
 
 
 def kernel_source_hash() -> str:
