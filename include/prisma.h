@@ -253,6 +253,20 @@ int prisma_gather_records(prisma_env_t* env, const int32_t* replica, const uint3
 int prisma_state_bytes(prisma_env_t* env, uint32_t* state_bytes,
                        uint32_t* lds_bytes);
 
+/* Sizing without a device: validates topo/params exactly as prisma_create
+ * does and reports the per-replica footprint (any pointer may be NULL). */
+typedef struct prisma_plan {
+    uint32_t state_bytes;       /* HBM state image per replica             */
+    uint32_t lds_bytes;         /* LDS per workgroup (= per replica)       */
+    uint32_t lds_state_bytes;   /* LDS part of the image                   */
+    uint32_t ring_entries;      /* packet slots over all link FIFOs        */
+    uint32_t record_bytes;      /* decision record size                    */
+    int32_t  obs_width;
+    int32_t  flow_slots;        /* register slots per lane (64 flows each) */
+    int32_t  link_slots;        /* register slots per lane (64 links each) */
+} prisma_plan_t;
+int prisma_plan(const prisma_topology_t* topo, const prisma_params_t* params, prisma_plan_t* out);
+
 void prisma_destroy(prisma_env_t* env);
 
 #ifdef __cplusplus

@@ -1576,6 +1576,23 @@ extern "C" int prisma_state_bytes(prisma_env_t* e, uint32_t* state_bytes, uint32
     return PRISMA_OK;
 }
 
+extern "C" int prisma_plan(const prisma_topology_t* topo, const prisma_params_t* params, prisma_plan_t* out) {
+    if (!topo || !params || !out) return set_err(PRISMA_ERR_ARG, "null argument");
+    Layout L;
+    std::vector<unsigned char> img;
+    int rc = build_layout(topo, params, L, img);
+    if (rc) return rc;
+    out->state_bytes = L.state_bytes;
+    out->lds_bytes = L.lds_bytes;
+    out->lds_state_bytes = L.lds_state_bytes;
+    out->ring_entries = (uint32_t)L.E * L.qcap_s + (uint32_t)L.N * L.qcap_a;
+    out->record_bytes = L.rec_bytes;
+    out->obs_width = L.W;
+    out->flow_slots = L.FS;
+    out->link_slots = L.LS;
+    return PRISMA_OK;
+}
+
 extern "C" void prisma_destroy(prisma_env_t* e) {
     if (!e) return;
     (void)hipSetDevice(e->device);

@@ -47,10 +47,16 @@ class _LogView(C.Structure):
                 ("obs_width", C.c_int32), ("n_replicas", C.c_int32)]
 
 
+class _Plan(C.Structure):
+    _fields_ = [("state_bytes", C.c_uint32), ("lds_bytes", C.c_uint32), ("lds_state_bytes", C.c_uint32),
+                ("ring_entries", C.c_uint32), ("record_bytes", C.c_uint32), ("obs_width", C.c_int32),
+                ("flow_slots", C.c_int32), ("link_slots", C.c_int32)]
+
+
 EXPORTS = [
     "prisma_abi_version", "prisma_last_error", "prisma_create", "prisma_reset", "prisma_step", "prisma_run",
     "prisma_read_counters", "prisma_counters_device", "prisma_log_view", "prisma_copy_log",
-    "prisma_copy_counters", "prisma_gather_records", "prisma_state_bytes", "prisma_destroy",
+    "prisma_copy_counters", "prisma_gather_records", "prisma_state_bytes", "prisma_plan", "prisma_destroy",
 ]
 
 _lib = None
@@ -91,6 +97,8 @@ def load_library(path: str = None):
     L.prisma_gather_records.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
     L.prisma_state_bytes.restype = C.c_int
     L.prisma_state_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    L.prisma_plan.restype = C.c_int
+    L.prisma_plan.argtypes = [C.POINTER(_Topo), C.POINTER(_Params), C.POINTER(_Plan)]
     L.prisma_destroy.restype = None
     L.prisma_destroy.argtypes = [C.c_void_p]
     if L.prisma_abi_version() != 3:
@@ -112,6 +120,27 @@ def _stream_handle(stream) -> Optional[int]:
     return int(stream.cuda_stream)
 
 
+def _topo_struct(topo: Topology):
+    keep = [np.ascontiguousarray(topo.row_ptr, dtype=np.int32),
+            np.ascontiguousarray(topo.link_dst, dtype=np.int32),
+            np.ascontiguousarray(topo.link_rev, dtype=np.int32),
+            np.ascontiguousarray(topo.flow_src, dtype=np.int32),
+            np.ascontiguousarray(topo.flow_dst, dtype=np.int32),
+            np.ascontiguousarray(topo.flow_rate_bps, dtype=np.uint64)]
+    t = _Topo(topo.n_nodes, topo.n_links, topo.n_flows, topo.max_deg, *[a.ctypes.data for a in keep])
+    return t, keep
+
+
+def plan(topo: Topology, params: dict) -> dict:
+    """prisma_plan: validate a scenario and report its per-replica footprint (no device needed)."""
+    L = load_library()
+    t, keep = _topo_struct(topo)
+    p = _Params(**{k: params[k] for k, _ in _Params._fields_})
+    out = _Plan()
+    _check(L.prisma_plan(C.byref(t), C.byref(p), C.byref(out)))
+    return {k: int(getattr(out, k)) for k, _ in _Plan._fields_}
+
+
 class PrismaEngine:
     """R replicas of one scenario on one MI355X (device memory owned by the library)."""
 
@@ -125,14 +154,7 @@ class PrismaEngine:
         self.R = int(n_replicas)
         self.device = int(device)
         self.torch_device = torch.device("cuda", self.device)
-        self._keep = [np.ascontiguousarray(topo.row_ptr, dtype=np.int32),
-                      np.ascontiguousarray(topo.link_dst, dtype=np.int32),
-                      np.ascontiguousarray(topo.link_rev, dtype=np.int32),
-                      np.ascontiguousarray(topo.flow_src, dtype=np.int32),
-                      np.ascontiguousarray(topo.flow_dst, dtype=np.int32),
-                      np.ascontiguousarray(topo.flow_rate_bps, dtype=np.uint64)]
-        t = _Topo(topo.n_nodes, topo.n_links, topo.n_flows, topo.max_deg,
-                  *[a.ctypes.data for a in self._keep])
+        t, self._keep = _topo_struct(topo)
         p = _Params(**{k: params[k] for k, _ in _Params._fields_})
         h = C.c_void_p()
         with torch.cuda.device(self.device):

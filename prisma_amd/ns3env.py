@@ -5,8 +5,9 @@ The reference runs one ns-3 process and, per overlay node, one
 debug)`` client (forwarder.py:47) that a Forwarder thread drives with
 ``reset()`` / ``step(action)`` (forwarder.py:291-332; ns3env.py:378-440):
 
-* the constructor blocks until the simulator first notifies this node, and
-  ``reset()`` returns that observation;
+* the constructor returns with the start-up state ([-1]) that every node's
+  environment notifies during setup (sim.cc:546); the action answering it is
+  ignored, and ``reset()`` returns that observation;
 * ``step(action)`` applies the action to the packet this node was last shown,
   then blocks until the simulator notifies this node again and returns
   ``(obs, reward, done, info)``: obs = ``[dst, v_0..v_{deg-1}]``
@@ -204,7 +205,13 @@ class _BridgeShim:
 
 
 class Ns3Env:
-    """ns3env.Ns3Env signature; node = port - session.base_port."""
+    """ns3env.Ns3Env signature; node = port - session.base_port.
+
+    Like the reference, the constructor returns at once with the start-up
+    state every node's PacketRoutingEnv::initialize() notifies (sim.cc:546,
+    packet-routing-gym.cc:216-219): obs [-1], reward -1, not done, info "-1,".
+    The action answering it is ignored (ExecuteActions with the train-step
+    flag, :200-201); later steps answer real data notifications."""
 
     def __init__(self, stepTime=0, port=0, startSim=True, simSeed=0, simArgs={}, debug=False,
                  session: Optional[PrismaSession] = None):
@@ -217,13 +224,13 @@ class Ns3Env:
         self.observation_space = Box(0, 16260, (1 + deg,))
         self.ns3ZmqBridge = _BridgeShim(self)
         self.connected = True
-        self._state = self._to_state(self.session._wait_for(self.node))
+        self._startup = True
+        self._state = ([-1], -1.0, False, "-1,")
 
     def _to_state(self, st):
         if st is None:
             self.connected = False
-            prev = getattr(self, "_state", None)
-            return prev if prev is not None else ([-1], 1.0, True, "")
+            return self._state
         v, obs, done, info = st
         return (list(obs), 1.0, bool(done), info)
 
@@ -231,7 +238,12 @@ class Ns3Env:
         return self._state[0]
 
     def step(self, action):
-        self._state = self._to_state(self.session._step_node(self.node, int(action)))
+        if self._startup:                    # the answer to the start-up state does nothing
+            self._startup = False
+            st = self.session._wait_for(self.node)
+        else:
+            st = self.session._step_node(self.node, int(action))
+        self._state = self._to_state(st)
         return self._state
 
     def close(self):

@@ -88,3 +88,32 @@ def test_engine_refuses_without_gpu():
     t = Topology.example("abilene")
     with pytest.raises(engine.PrismaError):
         engine.PrismaEngine(t, engine_params(t), 4)
+
+
+def test_plan_sizes_and_limits_without_a_device():
+    """prisma_plan validates like prisma_create and reports the footprint."""
+    from prisma_amd.config import engine_params
+    from prisma_amd.topology import Topology
+    ab = Topology.example("abilene")
+    p = engine.plan(ab, engine_params(ab))
+    assert p["obs_width"] == 4 and p["record_bytes"] == 48
+    assert (p["flow_slots"], p["link_slots"]) == (2, 1)
+    assert p["lds_bytes"] <= 10 * 1024                 # 16 replicas per CU (160 KiB LDS)
+    assert p["ring_entries"] == 28 * 44 + 11 * 8
+    ge = Topology.example("geant")
+    g = engine.plan(ge, engine_params(ge))
+    assert (g["flow_slots"], g["link_slots"]) == (8, 2) and g["obs_width"] == 8
+    assert g["lds_bytes"] <= 20 * 1024                 # 8 replicas per CU
+    # errors are status codes with a message, never exits
+    with pytest.raises(engine.PrismaError, match="log_capacity"):
+        engine.plan(ab, dict(engine_params(ab), log_capacity=1000))
+    with pytest.raises(engine.PrismaError, match="sim_time_s"):
+        engine.plan(ab, dict(engine_params(ab), sim_time_s=5000.0))
+    ring = np.zeros((300, 300), dtype=int)
+    for i in range(300):
+        ring[i, (i + 1) % 300] = ring[(i + 1) % 300, i] = 1
+    tm = np.zeros((300, 300), dtype=object)
+    tm[0, 1] = 1000
+    big = Topology.from_matrices(ring, tm)
+    with pytest.raises(engine.PrismaError, match="n_nodes"):
+        engine.plan(big, engine_params(big))

@@ -105,10 +105,15 @@ def test_threaded_per_node_envs(oracle_mod):
     seen = {u: [] for u in range(topo.n_nodes)}
     errors = []
 
+    # the reference builds every node's env in the main thread first (main.py:118-127)
+    envs = [Ns3Env(port=7100 + u, stepTime=0, startSim=0, simSeed=100) for u in range(topo.n_nodes)]
+
     def forwarder(u):
         try:
-            env = Ns3Env(port=7100 + u, stepTime=0, startSim=0, simSeed=100)
+            env = envs[u]
             obs = env.reset()
+            assert obs == [-1]
+            obs, _, done, info = env.step(0)        # start-up state: the answer is ignored
             while env.connected:
                 seen[u].append(list(obs))
                 obs, _, done, info = env.step(pol(u, obs))
