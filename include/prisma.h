@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PRISMA_ABI_VERSION 3
+#define PRISMA_ABI_VERSION 4
 
 /* status codes */
 #define PRISMA_OK              0
@@ -113,13 +113,18 @@ typedef struct prisma_params {
     double   loss_penalty;      /* ((16260+542)*8/cap+0.001)*N             */
     uint64_t seed;              /* simSeed                     [100]       */
     uint32_t replica_base;      /* global id of replica 0 (multi-GPU)      */
-    uint32_t log_capacity;      /* records kept per replica (power of 2,
-                                   >= 1024; must exceed the decisions made
-                                   while one packet crosses one link)      */
+    uint32_t log_capacity;      /* records kept per replica (power of 2 in
+                                   [1024, 2^22]; must exceed the decisions
+                                   made while one packet crosses one link) */
     uint32_t notify_dest;       /* prisma_step also stops at arrivals at the
-                                   destination (done=True notifications the
-                                   reference hands to the agent; the action
-                                   given for them is ignored)              */
+                                   destination (done=True notifications) and
+                                   at small-signalling arrivals (control:
+                                   obs [1000, signalled uid]); the action
+                                   given for them is ignored               */
+    uint32_t train;             /* --train: every data notification at a
+                                   non-source node echoes a 30-B small-
+                                   signalling packet to its last hop
+                                   (data-packet-manager.cc:301-347)        */
 } prisma_params_t;
 
 /*

@@ -33,7 +33,7 @@ class OrConfig(C.Structure):
         ("packet_size", C.c_uint32), ("sim_time_s", C.c_double), ("ping_interval_s", C.c_float),
         ("ma_size", C.c_uint32), ("ping_as_obs", C.c_uint32), ("auto_reset", C.c_uint32),
         ("loss_penalty", C.c_double), ("seed", C.c_uint64), ("replica", C.c_uint32),
-        ("episode", C.c_uint32), ("notify_dest", C.c_uint32),
+        ("episode", C.c_uint32), ("notify_dest", C.c_uint32), ("train", C.c_uint32),
     ]
 
 
@@ -52,6 +52,8 @@ def lib():
         L.or_step.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
         L.or_run_table.restype = C.c_int64
         L.or_run_table.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.or_pending_node.restype = C.c_int32
+        L.or_pending_node.argtypes = [C.c_void_p]
         L.or_record_count.restype = C.c_int64
         L.or_record_count.argtypes = [C.c_void_p]
         L.or_obs_width.restype = C.c_int32
@@ -123,6 +125,7 @@ class OracleSim:
         cfg.replica = int(replica)
         cfg.episode = int(episode)
         cfg.notify_dest = int(params.get("notify_dest", 0))
+        cfg.train = int(params.get("train", 0))
         self._cfg = cfg
         self.W = topo.obs_width
         self.rec_dtype = record_dtype(self.W)
@@ -170,6 +173,9 @@ class OracleSim:
         out = np.zeros((n, 4), dtype=np.int64)
         lib().or_copy_trace(self.h, 0, n, out.ctypes.data)
         return out
+
+    def pending_node(self) -> int:
+        return int(lib().or_pending_node(self.h))
 
     def last_info(self) -> str:
         buf = C.create_string_buffer(8192)

@@ -126,7 +126,7 @@ typedef struct {
 } counters_t;
 
 enum { ST_PENDING = 0, ST_ENQUEUED = 1, ST_DROPPED = 2, ST_DEST = 3, ST_DISCARDED = 4 };
-enum { DATA_PACKET = 0, PING_FORWARD_PACKET = 3, PING_BACK_PACKET = 4 };   /* enum-and-constants.h:5-11 */
+enum { DATA_PACKET = 0, SMALL_SIGN_PACKET = 2, PING_FORWARD_PACKET = 3, PING_BACK_PACKET = 4 };   /* enum-and-constants.h:5-11 */
 enum { EV_PING = 0, EV_START = 1, EV_SEND = 2, EV_COMPLETE = 3, EV_RECEIVE = 4 };
 
 /* ------------------------------------------------------------------ */
@@ -187,7 +187,7 @@ struct or_sim {
     /* records */
     unsigned char* rec; int64_t rec_n, rec_cap; int rec_bytes;
     /* pending decision */
-    int pend; int pend_pkt, pend_node, pend_link; int64_t pend_rec; int pend_dest;
+    int pend; int pend_pkt, pend_node, pend_link; int64_t pend_rec; int pend_dest; int pend_ctrl;
     int over;
     /* trace */
     int trace_on; int64_t* tr; int64_t tr_n, tr_cap;
@@ -445,6 +445,31 @@ static void build_info(or_sim_t* s, const pkt_t* k, int v) {
     snprintf(b + n, cap - n, ", Source=%d, Destination=%d, node=%d", k->src, k->dst, v);
 }
 
+/* small-signalling info: PacketManager::getInfo (tokens 0-17) +
+ * SmallSignalingPacketManager::getInfo (small-signaling-packet-manager.cc:104-114).
+ * Token 3 (the ns-3 packet uid of the echo) is not modelled: it carries the
+ * signalled data packet's uid, as token 18 does. */
+static void build_ctrl_info(or_sim_t* s, const pkt_t* k, int v) {
+    char* b = s->info;
+    size_t cap = sizeof(s->info), n = 0;
+    double now = get_seconds(s->now);
+    float avg_e2e = s->cnt.e2e_n ? s->cnt.e2e_sum / (float)s->cnt.e2e_n : 0.0f;
+    float avg_cost = s->cnt.cost_n ? s->cnt.cost_sum / (float)s->cnt.cost_n : 0.0f;
+    float sig = s->cnt.bytes_data ? (float)s->cnt.bytes_signaling / (float)s->cnt.bytes_data : 0.0f;
+    n += snprintf(b + n, cap - n, "End to End Delay=%f, Packet Size=%u, Current sim time =%f, Pkt ID =%u, packetType =%d",
+                  now - (double)k->start_time, k->size, now, k->uid, k->type);
+    n += snprintf(b + n, cap - n, ", Avg End to End Delay =%f, Avg Cost =%f, Avg Underlay End to End Delay =%f, Avg Underlay Cost =%f",
+                  (double)avg_e2e, (double)avg_cost, 0.0, 0.0);
+    n += snprintf(b + n, cap - n, ", Packets dropped =%d, Packets delivered =%d, Packets injected =%d,Packets Buffered =%d",
+                  s->cnt.ov_lost, s->cnt.ov_arrived, s->cnt.ov_injected,
+                  s->cnt.ov_injected - (s->cnt.ov_arrived + s->cnt.ov_lost));
+    n += snprintf(b + n, cap - n, ", Packets dropped Underlay =%d, Packets delivered Underlay=%d, Packets injected Underlay=%d,Packets Buffered Underlay=%d",
+                  s->cnt.un_lost, s->cnt.un_arrived, s->cnt.un_injected,
+                  s->cnt.un_injected - (s->cnt.un_arrived + s->cnt.un_lost));
+    n += snprintf(b + n, cap - n, ",Signaling overhead =%f", (double)sig);
+    snprintf(b + n, cap - n, ", PacketIdSignaled=%u, Arrived at final dest=%d", k->uid, (int)(k->dst == v));
+}
+
 /* ------------------------------------------------------------------ */
 /* event handlers                                                      */
 /* ------------------------------------------------------------------ */
@@ -502,6 +527,24 @@ static void ping_back_receive(or_sim_t* s, int l_in, int p) {       /* ping-back
     VEC_PUSH(dv, k->one_hop_delay);
 }
 
+/* DataPacketManager::sendSmallSignalingPacket (data-packet-manager.cc:301-347),
+ * called from ExecuteActions before sendPacket when --train (packet-routing-gym.cc:203-206):
+ * a 0-B payload (30 B on the wire, signalling type "ideal") back on the device the data
+ * packet arrived on, to its last hop; not sent at the packet's source node. */
+static void send_small_signaling(or_sim_t* s, const pkt_t* data, int v, int l_in) {
+    if (!s->c.train || data->src == v) return;
+    int q = pkt_alloc(s);
+    pkt_t* e = &s->pk[q];
+    e->type = SMALL_SIGN_PACKET;
+    e->dst = e->next_hop = data->last_hop;
+    e->last_hop = e->src = v;
+    e->uid = data->uid;                               /* SetIdValue(m_packetUid) */
+    e->start_time = 0;
+    e->valable = 0;
+    e->size = 0 + 8 + 20 + 2;
+    dev_send(s, s->c.link_rev[l_in], q);               /* m_receivingNetDev->Send */
+}
+
 static void flow_schedule_next(or_sim_t* s, int f) {                /* poisson-application.cc:265-295 */
     uint32_t key[2] = { (uint32_t)s->c.seed, s->c.replica };
     uint32_t ctr[4] = { (uint32_t)f, (uint32_t)s->flow_draws[f], s->c.episode, 1u };
@@ -554,14 +597,24 @@ static void receive_counters(or_sim_t* s, const pkt_t* k, int v) {
 static void finish_data_decision(or_sim_t* s, int action) {
     int p = s->pend_pkt, v = s->pend_node;
     int64_t d = s->pend_rec;
-    if (s->pend_dest) {                 /* done=True notification: sendPacket does nothing (:256-260) */
+    if (s->pend_ctrl) {                 /* control notification: ExecuteActions sends nothing */
         receive_counters(s, &s->pk[p], v);
+        pkt_free(s, p);
+        s->pend = 0;
+        s->pend_ctrl = 0;
+        return;
+    }
+    if (s->pend_dest) {                 /* done=True notification: sendPacket does nothing (:256-260) */
+        pkt_t orig = s->pk[p];
+        send_small_signaling(s, &orig, v, s->pend_link);
+        receive_counters(s, &orig, v);
         pkt_free(s, p);
         s->pend = 0;
         s->pend_dest = 0;
         return;
     }
     pkt_t orig = s->pk[p];
+    send_small_signaling(s, &orig, v, s->pend_link);
     int deg = s->c.row_ptr[v + 1] - s->c.row_ptr[v];
     rec_head_t* r = rec_at(s, d);
     r->action = (int8_t)action;
@@ -629,13 +682,26 @@ static int receive(or_sim_t* s, int di, int p) {
                 s->pend = 1; s->pend_dest = 1; s->pend_pkt = p; s->pend_node = v; s->pend_link = di; s->pend_rec = dn;
                 return 1;
             }
-            receive_counters(s, k, v);                                /* sendPacket does nothing */
+            pkt_t orig = *k;
+            send_small_signaling(s, &orig, v, di);
+            receive_counters(s, &orig, v);                            /* sendPacket does nothing */
             pkt_free(s, p);
             return 0;
         }
         r->status = ST_PENDING;
         s->pend = 1; s->pend_pkt = p; s->pend_node = v; s->pend_link = di; s->pend_rec = dn;
         return 1;
+    }
+    if (k->type == SMALL_SIGN_PACKET) {
+        /* SmallSignalingPacketManager::receivePacket (small-signaling-packet-manager.cc:86-94):
+         * valid (nextHop == node and arrived at its final destination) -> Notify */
+        if (k->next_hop == v && k->dst == v) {
+            build_ctrl_info(s, k, v);
+            if (s->c.notify_dest) {
+                s->pend = 1; s->pend_ctrl = 1; s->pend_pkt = p; s->pend_node = v; s->pend_link = di;
+                return 1;
+            }
+        }
     }
     if (k->type == PING_FORWARD_PACKET) ping_forward_receive(s, di, p);
     else if (k->type == PING_BACK_PACKET) ping_back_receive(s, di, p);
@@ -734,6 +800,12 @@ void or_destroy(or_sim_t* s) {
 int or_step(or_sim_t* s, int32_t action, int32_t* obs_out) {
     if (s->pend) finish_data_decision(s, action);
     int r = run_until_decision(s);
+    if (r && obs_out && s->pend_ctrl) {             /* GetObservation for a control packet: [1000] */
+        for (int i = 0; i < s->W; ++i) obs_out[i] = 0;
+        obs_out[0] = 1000;
+        obs_out[1] = (int32_t)s->pk[s->pend_pkt].uid;  /* the signalled uid (engine ABI: obs[1]) */
+        return r;
+    }
     if (r && obs_out) {
         const uint32_t* o = (const uint32_t*)((unsigned char*)rec_at(s, s->pend_rec) + sizeof(rec_head_t));
         for (int i = 0; i < s->W; ++i) obs_out[i] = (int32_t)o[i];
@@ -755,6 +827,7 @@ int64_t or_run_table(or_sim_t* s, const uint8_t* table, int64_t max_hops) {
 }
 
 int64_t or_record_count(const or_sim_t* s) { return s->rec_n; }
+int32_t or_pending_node(const or_sim_t* s) { return s->pend ? s->pend_node : -1; }
 int32_t or_obs_width(const or_sim_t* s) { return s->W; }
 
 int64_t or_copy_records(const or_sim_t* s, int64_t first, int64_t count, void* out) {

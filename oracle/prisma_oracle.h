@@ -43,8 +43,11 @@ typedef struct or_config {
     uint64_t seed;
     uint32_t replica;           /* global replica id (Philox key word 1)   */
     uint32_t episode;
-    uint32_t notify_dest;       /* or_step also stops at destination
-                                   notifications (their action is ignored) */
+    uint32_t notify_dest;       /* or_step also stops at destination and
+                                   control (small-signalling) notifications;
+                                   their action is ignored                 */
+    uint32_t train;             /* --train: small-signalling echo per data
+                                   notification at a non-source node       */
 } or_config_t;
 
 typedef struct or_sim or_sim_t;
@@ -57,6 +60,9 @@ void      or_destroy(or_sim_t* s);
  * decision is pending (obs written to obs_out[obs_width]), 0 if the episode
  * is over. */
 int or_step(or_sim_t* s, int32_t action, int32_t* obs_out);
+
+/* Node of the pending notification (-1 if none). */
+int32_t or_pending_node(const or_sim_t* s);
 
 /* Run with a [N][N] action table until `max_hops` more hops were executed
  * or the episode ended.  Returns hops executed. */

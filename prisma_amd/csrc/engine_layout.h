@@ -12,19 +12,27 @@ constexpr int kWave = 64;
 constexpr uint32_t K_PING = 0u, K_FLOW = 1u, K_COMPLETE = 2u, K_ARRIVE = 3u;
 
 // 4-byte packet entry of a link ring; type in bits 0-1:
-//   T_RELAY  data packet forwarded by a decision: bits 2-31 = that decision's
-//            index mod 2^30 (its uid, destination, start second and decision
-//            time are read back from the decision record in the HBM log)
+//   T_RELAY  data packet forwarded by a decision: bits 2-23 = that decision's
+//            index mod 2^22, bits 24-31 = the packet's source node (its uid,
+//            destination, start second and decision time are read back from
+//            the decision record in the HBM log)
 //   T_FRESH  data packet of a flow app on its access link: bits 2-10 flow,
 //            bit 11 parity of the start second, bits 12-31 uid mod 2^20
 //   T_PFWD / T_PBACK  ping forward / back (enum-and-constants.h:5-11):
-//            bits 2-8 tunnel, bits 9-31 round; the one-hop delay a ping-back
+//            bits 2-8 tunnel, bits 9-30 round; the one-hop delay a ping-back
 //            carries sits in a per-tunnel side table (Layout::s_pbd)
+//   echo     small-signalling packet (--train): T_PBACK with bit 31 set,
+//            bits 9-30 = the signalled data packet's uid mod 2^22
 constexpr uint32_t T_RELAY = 0u, T_FRESH = 1u, T_PFWD = 2u, T_PBACK = 3u;
+constexpr uint32_t kEchoBit = 1u << 31;
 __host__ __device__ inline uint32_t ent_type(uint32_t x) { return x & 3u; }
 __host__ __device__ inline bool ent_is_data(uint32_t x) { return (x & 2u) == 0u; }
-__host__ __device__ inline uint32_t r_make(uint32_t dec) { return T_RELAY | (dec << 2); }
-__host__ __device__ inline uint32_t r_dec(uint32_t x) { return x >> 2; }
+__host__ __device__ inline bool ent_is_echo(uint32_t x) { return (x & (kEchoBit | 3u)) == (kEchoBit | T_PBACK); }
+__host__ __device__ inline uint32_t r_make(uint32_t dec, uint32_t src) {
+    return T_RELAY | ((dec & ((1u << 22) - 1u)) << 2) | (src << 24);
+}
+__host__ __device__ inline uint32_t r_dec(uint32_t x) { return (x >> 2) & ((1u << 22) - 1u); }
+__host__ __device__ inline uint32_t r_src(uint32_t x) { return x >> 24; }
 __host__ __device__ inline uint32_t f_make(uint32_t flow, uint32_t start_parity, uint32_t uid) {
     return T_FRESH | (flow << 2) | (start_parity << 11) | (uid << 12);
 }
@@ -35,8 +43,13 @@ __host__ __device__ inline uint32_t p_make(uint32_t type, uint32_t tunnel, uint3
     return type | (tunnel << 2) | (round << 9);
 }
 __host__ __device__ inline uint32_t p_tunnel(uint32_t x) { return (x >> 2) & 127u; }
-__host__ __device__ inline uint32_t p_round(uint32_t x) { return x >> 9; }
-constexpr uint32_t kRelayMask = (1u << 30) - 1u, kUidMask = (1u << 20) - 1u;
+__host__ __device__ inline uint32_t p_round(uint32_t x) { return (x >> 9) & ((1u << 22) - 1u); }
+__host__ __device__ inline uint32_t e_make(uint32_t uid) { return T_PBACK | kEchoBit | ((uid & ((1u << 22) - 1u)) << 9); }
+__host__ __device__ inline uint32_t e_uid(uint32_t x) { return (x >> 9) & ((1u << 22) - 1u); }
+constexpr uint32_t kRelayMask = (1u << 22) - 1u, kUidMask = (1u << 20) - 1u;
+
+// pending-notification flags (Hdr::pend_ent[3])
+constexpr uint32_t PEND_DEST = 1u, PEND_ECHO = 2u, PEND_CTRL = 4u;
 
 struct Hdr {                 // 128 bytes at state offset 0
     int64_t  now;
@@ -49,7 +62,7 @@ struct Hdr {                 // 128 bytes at state offset 0
     uint32_t pend_link;
     uint32_t pend_node;
     uint32_t pend_dec;
-    uint32_t pend_ent[4];    // entry, dst, start second, 1 = destination notification
+    uint32_t pend_ent[4];    // entry, dst, start second, PEND_* flags
     uint32_t ping_rounds;
     uint32_t episode;
     uint32_t over;
@@ -58,7 +71,8 @@ struct Hdr {                 // 128 bytes at state offset 0
     uint32_t hops_launch;
     uint64_t hops_total;
     uint64_t events_total;
-    uint32_t pad[6];
+    uint32_t pend_uid;       // uid of the pending data packet (echo payload)
+    uint32_t pad[5];
 };
 static_assert(sizeof(Hdr) == 128, "Hdr size");
 // LDS offsets of the header, the counters (144 B) and the pending observation
@@ -89,12 +103,12 @@ struct Layout {
     uint32_t PBK;                // ping-back delay slots per tunnel (power of two)
     int32_t  FS, LS;             // flow / link register slots per lane
     // link constants (identical on every switch link: sim.cc:414-433)
-    int64_t  sw_txd, sw_txp, sw_prop;
+    int64_t  sw_txd, sw_txp, sw_txe, sw_prop;   // tx of data / ping / echo, propagation
     uint32_t qcap_s, qcap_a, qmax_bytes, acc_qmax_pkts;
     // scenario constants
     int64_t  t_end, ping_period;
-    uint32_t data_size, ping_size;
-    uint32_t ma, ping_as_obs, auto_reset, notify_dest;
+    uint32_t data_size, ping_size, echo_size;
+    uint32_t ma, ping_as_obs, auto_reset, notify_dest, train;
     uint32_t seed_lo, replica_base;
     uint32_t log_cap, rec_bytes;
     double   loss_penalty;

@@ -222,6 +222,7 @@ struct LV {
     __device__ __forceinline__ int32_t LS() const { return (int32_t)u(offsetof(Layout, LS) / 4); }
     __device__ __forceinline__ int64_t sw_txd() const { return mk64(u(offsetof(Layout, sw_txd) / 4), u(offsetof(Layout, sw_txd) / 4 + 1)); }
     __device__ __forceinline__ int64_t sw_txp() const { return mk64(u(offsetof(Layout, sw_txp) / 4), u(offsetof(Layout, sw_txp) / 4 + 1)); }
+    __device__ __forceinline__ int64_t sw_txe() const { return mk64(u(offsetof(Layout, sw_txe) / 4), u(offsetof(Layout, sw_txe) / 4 + 1)); }
     __device__ __forceinline__ int64_t sw_prop() const { return mk64(u(offsetof(Layout, sw_prop) / 4), u(offsetof(Layout, sw_prop) / 4 + 1)); }
     __device__ __forceinline__ uint32_t qcap_s() const { return (uint32_t)u(offsetof(Layout, qcap_s) / 4); }
     __device__ __forceinline__ uint32_t qcap_a() const { return (uint32_t)u(offsetof(Layout, qcap_a) / 4); }
@@ -231,10 +232,12 @@ struct LV {
     __device__ __forceinline__ int64_t ping_period() const { return mk64(u(offsetof(Layout, ping_period) / 4), u(offsetof(Layout, ping_period) / 4 + 1)); }
     __device__ __forceinline__ uint32_t data_size() const { return (uint32_t)u(offsetof(Layout, data_size) / 4); }
     __device__ __forceinline__ uint32_t ping_size() const { return (uint32_t)u(offsetof(Layout, ping_size) / 4); }
+    __device__ __forceinline__ uint32_t echo_size() const { return (uint32_t)u(offsetof(Layout, echo_size) / 4); }
     __device__ __forceinline__ uint32_t ma() const { return (uint32_t)u(offsetof(Layout, ma) / 4); }
     __device__ __forceinline__ uint32_t ping_as_obs() const { return (uint32_t)u(offsetof(Layout, ping_as_obs) / 4); }
     __device__ __forceinline__ uint32_t auto_reset() const { return (uint32_t)u(offsetof(Layout, auto_reset) / 4); }
     __device__ __forceinline__ uint32_t notify_dest() const { return (uint32_t)u(offsetof(Layout, notify_dest) / 4); }
+    __device__ __forceinline__ uint32_t train() const { return (uint32_t)u(offsetof(Layout, train) / 4); }
     __device__ __forceinline__ uint32_t seed_lo() const { return (uint32_t)u(offsetof(Layout, seed_lo) / 4); }
     __device__ __forceinline__ uint32_t replica_base() const { return (uint32_t)u(offsetof(Layout, replica_base) / 4); }
     __device__ __forceinline__ uint32_t log_cap() const { return (uint32_t)u(offsetof(Layout, log_cap) / 4); }
@@ -333,7 +336,7 @@ __device__ __forceinline__ bool key_less(int64_t t, uint32_t s, int64_t bt, uint
 }
 
 __device__ __forceinline__ uint32_t ent_size(const LV& L, uint32_t x) {
-    return ent_is_data(x) ? L.data_size() : L.ping_size();
+    return ent_is_data(x) ? L.data_size() : (ent_is_echo(x) ? L.echo_size() : L.ping_size());
 }
 __device__ __forceinline__ uint32_t ring_off(const LV& L, uint32_t l) {
     return l < (uint32_t)L.E() ? l * L.qcap_s() : (uint32_t)L.E() * L.qcap_s() + (l - (uint32_t)L.E()) * L.qcap_a();
@@ -391,7 +394,8 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
                                                uint32_t x) {
     const LV& L = S.lv;
     const bool sw = l < (uint32_t)L.E();
-    int64_t tx = sw ? (ent_is_data(x) ? L.sw_txd() : L.sw_txp()) : S.T->acctx[l - (uint32_t)L.E()];
+    int64_t tx = sw ? (ent_is_data(x) ? L.sw_txd() : (ent_is_echo(x) ? L.sw_txe() : L.sw_txp()))
+                    : S.T->acctx[l - (uint32_t)L.E()];
     int64_t prop = sw ? L.sw_prop() : 0;
     k.busy = 1;
     k.cp_t = lo32(H.now + tx);
@@ -554,11 +558,25 @@ __device__ __forceinline__ void receive_counters(const Sim& S, Regs<FS, LS>& R, 
         CNT_ADD(S, e2e_n, 1u);
     }
     // pings are always addressed to the node that receives them
-    if (!ent_is_data(x)) CNT_ADD(S, bytes_signaling, L.ping_size() - 2u);
+    if (!ent_is_data(x)) CNT_ADD(S, bytes_signaling, ent_size(L, x) - 2u);
     if (ent_type(x) == T_FRESH) {
         CNT_ADD(S, ov_injected, 1u);
         CNT_ADD(S, bytes_data, L.data_size() - 2u);
     }
+}
+
+constexpr uint32_t kNoLink = 0xffffffffu;
+
+// source node of a data entry (MyTag source)
+__device__ __forceinline__ uint32_t ent_src(const Sim& S, uint32_t x) {
+    return ent_type(x) == T_FRESH ? (uint32_t)S.T->fsrc[f_flow(x)] : r_src(x);
+}
+
+// DataPacketManager::sendSmallSignalingPacket (data-packet-manager.cc:301-347): a 0-B
+// payload (30 B on the wire, signalling type "ideal") back on the arrival device
+template <int FS, int LS>
+__device__ __forceinline__ void send_echo(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t link, uint32_t uid) {
+    if (!link_send(S, R, H, link, e_make(uid))) CNT_ADD(S, ctrl_dropped, 1u);
 }
 
 // DataPacketManager::sendPacket (data-packet-manager.cc:251-299) for decision
@@ -568,18 +586,22 @@ __device__ __forceinline__ void receive_counters(const Sim& S, Regs<FS, LS>& R, 
 template <int FS, int LS>
 __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t x, uint32_t dst,
                                                uint32_t start, uint32_t uid, uint32_t v, uint32_t d, int action,
-                                               bool fused, double reward, int32_t prev, uint32_t obs_reg) {
+                                               bool fused, double reward, int32_t prev, uint32_t obs_reg,
+                                               uint32_t echo_link) {
     const LV& L = S.lv;
 #if PRISMA_TIMING
     S.tlast = TM_NOW();
 #endif
+    // ExecuteActions (packet-routing-gym.cc:203-208): the --train echo goes first
+    if (echo_link != kNoLink) send_echo(S, R, H, echo_link, uid);
     int r0 = S.T->rowptr[v], deg = S.T->rowptr[v + 1] - r0;
     uint32_t status;
     if (action >= 0 && action < deg) {
         uint32_t l = (uint32_t)(r0 + action);
         CNT_ADD(S, hops, 1u);
         CNT_ADD(S, hop_deg_sum, (uint64_t)deg);
-        const uint32_t fwd = (PRISMA_ABLATE & 1) ? (T_RELAY | (dst << 2) | (start << 10)) : r_make(d);
+        const uint32_t src = ent_src(S, x);
+        const uint32_t fwd = (PRISMA_ABLATE & 1) ? (T_RELAY | (dst << 2) | (start << 10) | (src << 24)) : r_make(d, src);
         if (link_send(S, R, H, l, fwd)) {                         // lastHop = v, previous decision = d
             status = PRISMA_ST_ENQUEUED;
         } else {
@@ -603,18 +625,27 @@ __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Ho
 #endif
 }
 
-// returns 1 if a hop was executed (0 for a destination notification, whose
-// action is ignored: sendPacket at the destination does nothing, :256-260)
+// Answer to the pending notification.  Returns 1 if a hop was executed (0 for a
+// destination or control notification, whose action is ignored: sendPacket at
+// the destination does nothing (:256-260), ExecuteActions sends nothing for a
+// small-signalling packet).
 template <int FS, int LS>
 __device__ __forceinline__ int finish_pending(const Sim& S, Regs<FS, LS>& R, Hot& H, int action) {
     const Hdr& h = *S.h;
     H.pend = 0;
-    if (u_ld32(&h.pend_ent[3])) {
-        receive_counters(S, R, H, u_ld32(&h.pend_ent[0]), true, u_ld32(&h.pend_ent[2]));
+    const uint32_t x = u_ld32(&h.pend_ent[0]), flags = u_ld32(&h.pend_ent[3]);
+    if (flags & PEND_CTRL) {
+        receive_counters(S, R, H, x, false, 0u);
         return 0;
     }
-    apply_decision(S, R, H, u_ld32(&h.pend_ent[0]), 0u, 0u, 0u, u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action,
-                   false, 0.0, 0, 0u);
+    const uint32_t echo_link = (flags & PEND_ECHO) ? (uint32_t)S.T->lrev[u_ld32(&h.pend_link)] : kNoLink;
+    if (flags & PEND_DEST) {
+        if (echo_link != kNoLink) send_echo(S, R, H, echo_link, u_ld32(&h.pend_uid));
+        receive_counters(S, R, H, x, true, u_ld32(&h.pend_ent[2]));
+        return 0;
+    }
+    apply_decision(S, R, H, x, 0u, 0u, u_ld32(&h.pend_uid), u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action,
+                   false, 0.0, 0, 0u, echo_link);
     return 1;
 }
 
@@ -682,7 +713,7 @@ __device__ __forceinline__ void wire_pop(const Sim& S, Regs<FS, LS>& R, const Ho
 }
 
 struct Decision {
-    uint32_t x, dst, start, uid, v, d; double reward; int32_t prev; uint32_t obs, dest;
+    uint32_t x, dst, start, uid, v, d; double reward; int32_t prev; uint32_t obs, flags;
 };
 
 // returns 1 if a data decision needs an action
@@ -739,22 +770,36 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
         }
         const uint32_t o = (S.lane == 0) ? dst : obs_links;
         CNT_ADD(S, decisions, 1u);
-        D.dest = 0;
+        // --train: the answer to this notification also echoes a small-signalling
+        // packet to the last hop, unless this node is the packet's source (:303-306)
+        const uint32_t echo = (L.train() && v != ent_src(S, x)) ? PEND_ECHO : 0u;
+        D.x = x; D.dst = dst; D.start = start; D.uid = uid; D.v = v; D.d = d; D.reward = reward; D.prev = prev;
+        D.obs = o; D.flags = echo;
         if (dst == v) {                                             // getGameOver
             write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_DESTINATION, o);
             if (!fused && L.notify_dest()) {                        // the agent is notified (done=True)
-                D.x = x; D.dst = dst; D.start = start; D.v = v; D.d = d; D.obs = o; D.dest = 1;
+                D.flags |= PEND_DEST;
                 return 1;
             }
+            if (echo) send_echo(S, R, H, (uint32_t)S.T->lrev[l], uid);
             receive_counters(S, R, H, x, true, start);
             return 0;
         }
         if (!fused) write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_PENDING, o);
-        D.x = x; D.dst = dst; D.start = start; D.uid = uid; D.v = v; D.d = d; D.reward = reward; D.prev = prev;
-        D.obs = o;
         return 1;
     }
     wire_pop(S, R, H, l, k);
+    if (ent_is_echo(x)) {
+        // SmallSignalingPacketManager::receivePacket (small-signaling-packet-manager.cc:86-94):
+        // addressed to this node, so valid -> Notify; the agent sees obs [1000]
+        if (!fused && L.notify_dest()) {
+            D.x = x; D.v = v; D.uid = e_uid(x); D.flags = PEND_CTRL;
+            D.obs = (S.lane == 0) ? 1000u : ((S.lane == 1) ? e_uid(x) : 0u);
+            return 1;
+        }
+        receive_counters(S, R, H, x, false, 0u);
+        return 0;
+    }
     const uint32_t tun = p_tunnel(x), rnd = p_round(x);
     if (type == T_PFWD) {                                           // ping-forward-packet-manager.cc:94-156
         float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
@@ -1137,7 +1182,8 @@ prisma_step_kernel_t(KParams P) {
                 if (table_mode) {
                     int a = (int)S.table[D.v * NN + D.dst];
                     apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, (int)rfl((uint32_t)a), true,
-                                   D.reward, D.prev, D.obs);
+                                   D.reward, D.prev, D.obs,
+                                   (D.flags & PEND_ECHO) ? (uint32_t)S.T->lrev[id] : kNoLink);
                     H.hops_launch++;
                     if (H.hops_launch >= max_hops) H.stop = 1;
                     TM_MARK(2);
@@ -1145,7 +1191,8 @@ prisma_step_kernel_t(KParams P) {
                     if (lane == 0) {
                         Hdr& h = *S.h;
                         h.pend_link = id; h.pend_node = D.v; h.pend_dec = D.d;
-                        h.pend_ent[0] = D.x; h.pend_ent[1] = D.dst; h.pend_ent[2] = D.start; h.pend_ent[3] = D.dest;
+                        h.pend_ent[0] = D.x; h.pend_ent[1] = D.dst; h.pend_ent[2] = D.start; h.pend_ent[3] = D.flags;
+                        h.pend_uid = D.uid;
                     }
                     if (lane < L.W()) S.obs[lane] = D.obs;
                     H.pend = 1;
@@ -1287,7 +1334,7 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
         return set_err(PRISMA_ERR_CONFIG, "sim_time_s must be in (0, 4095] (12-bit packet start second)");
     if (P->sim_time_s / (double)P->ping_interval_s >= (double)(1u << 21))
         return set_err(PRISMA_ERR_CONFIG, "more than 2^21 ping rounds per episode (21-bit round index)");
-    if (P->log_capacity < 1024 || (P->log_capacity & (P->log_capacity - 1)))
+    if (P->log_capacity < 1024 || P->log_capacity > (1u << 22) || (P->log_capacity & (P->log_capacity - 1)))
         return set_err(PRISMA_ERR_CONFIG, "log_capacity must be a power of two >= 1024");
 
     memset(&L, 0, sizeof(L));
@@ -1297,9 +1344,12 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.MA = (int)P->ma_size;
     L.data_size = P->packet_size + 30u;             // UDP 8 + IP 20 + PPP 2
     L.ping_size = 8u + 30u;
+    L.echo_size = 0u + 30u;                         // signalling type "ideal": 0-B payload (sim.cc:371-391)
+    L.train = P->train ? 1u : 0u;
     // link constants (sim.cc:398-433): switch links share rate, delay and queue
     L.sw_txd = sec_to_ns((double)L.data_size * 8 / (double)P->link_bps);
     L.sw_txp = sec_to_ns((double)L.ping_size * 8 / (double)P->link_bps);
+    L.sw_txe = sec_to_ns((double)L.echo_size * 8 / (double)P->link_bps);
     L.sw_prop = P->link_delay_ns;
     L.qmax_bytes = P->max_buffer_bytes;
     L.acc_qmax_pkts = 1000u;                        // "1000p" packet-mode access queue
@@ -1314,8 +1364,9 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     }
     // wire capacity: packets whose transmission ended within the last
     // propagation delay, plus the one being transmitted
-    if (L.sw_txp < 1) return set_err(PRISMA_ERR_CONFIG, "link too fast for the wire model");
-    uint32_t wire = (uint32_t)(P->link_delay_ns / L.sw_txp) + 2u;
+    const int64_t min_tx = L.train ? L.sw_txe : L.sw_txp;      // shortest packet on a switch link
+    if (min_tx < 1) return set_err(PRISMA_ERR_CONFIG, "link too fast for the wire model");
+    uint32_t wire = (uint32_t)(P->link_delay_ns / min_tx) + 2u;
     L.WCAP = (int)next_pow2(wire < 2 ? 2 : wire);
     if (L.WCAP > 64) return set_err(PRISMA_ERR_CONFIG, "propagation delay too long for the wire model");
     // ring capacity: full byte-limited FIFO of data + the control packets that
@@ -1323,7 +1374,11 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     double drain_s = (double)P->max_buffer_bytes * 8.0 / (double)P->link_bps + (double)L.sw_txd * 1e-9;
     double span = 2.0 * drain_s + 2.0 * (double)P->link_delay_ns * 1e-9;
     uint32_t ctrl = 2u * ((uint32_t)(span / (double)P->ping_interval_s) + 3u);
-    uint32_t qs = P->max_buffer_bytes / L.data_size + ctrl + (uint32_t)L.WCAP;
+    // --train echoes on a link answer data packets that crossed the reverse link,
+    // which arrive at least one data transmission apart: at most drain/tx_data + 2
+    // of them wait in a FIFO at once
+    uint32_t echoes = L.train ? (uint32_t)(drain_s / ((double)L.sw_txd * 1e-9)) + 2u : 0u;
+    uint32_t qs = P->max_buffer_bytes / L.data_size + ctrl + echoes + (uint32_t)L.WCAP;
     qs = (qs + (uint32_t)L.WCAP - 1) / (uint32_t)L.WCAP * (uint32_t)L.WCAP;
     if (qs > 65535u) return set_err(PRISMA_ERR_CONFIG, "queue too deep");
     L.qcap_s = qs;

@@ -38,7 +38,7 @@ class _Params(C.Structure):
         ("packet_size", C.c_uint32), ("sim_time_s", C.c_double), ("ping_interval_s", C.c_float),
         ("ma_size", C.c_uint32), ("ping_as_obs", C.c_uint32), ("auto_reset", C.c_uint32),
         ("loss_penalty", C.c_double), ("seed", C.c_uint64), ("replica_base", C.c_uint32),
-        ("log_capacity", C.c_uint32), ("notify_dest", C.c_uint32),
+        ("log_capacity", C.c_uint32), ("notify_dest", C.c_uint32), ("train", C.c_uint32),
     ]
 
 
@@ -101,7 +101,7 @@ def load_library(path: str = None):
     L.prisma_plan.argtypes = [C.POINTER(_Topo), C.POINTER(_Params), C.POINTER(_Plan)]
     L.prisma_destroy.restype = None
     L.prisma_destroy.argtypes = [C.c_void_p]
-    if L.prisma_abi_version() != 3:
+    if L.prisma_abi_version() != 4:
         raise PrismaError("libprisma_amd ABI version mismatch")
     _lib = L
     return L

@@ -70,10 +70,9 @@ class InfoTracker:
         elif st == ST_DESTINATION:
             self.src.pop(int(rec["uid"]), None)
 
-    def render(self, rec, cnt) -> str:
-        """DataPacketManager::getInfo for the notified data packet (22 tokens)."""
-        v = int(rec["node"])
-        now = int(rec["t_ns"]) / 1e9
+    @staticmethod
+    def _stats(cnt, now: float, start: float, size: int, uid: int, ptype: int) -> str:
+        """PacketManager::getInfo tokens 0-17 (packet-manager.cc:119-176)."""
         e2e_n, cost_n = int(cnt["e2e_n"]), int(cnt["cost_n"])
         avg_e2e = np.float32(cnt["e2e_sum"]) / np.float32(e2e_n) if e2e_n else np.float32(0.0)
         avg_cost = np.float32(cnt["cost_sum"]) / np.float32(cost_n) if cost_n else np.float32(0.0)
@@ -81,21 +80,33 @@ class InfoTracker:
         sig = np.float32(int(cnt["bytes_signaling"])) / np.float32(bd) if bd else np.float32(0.0)
         lost, inj, arr = int(cnt["ov_lost"]), int(cnt["ov_injected"]), int(cnt["ov_arrived"])
         ul, ui, ua = int(cnt["un_lost"]), int(cnt["un_injected"]), int(cnt["un_arrived"])
-        lv = self.lost[v]
-        lost_ids = "".join("%u;" % u for u in reversed(lv))
-        lv.clear()
-        uid = int(rec["uid"])
-        src = self.src.get(uid, v)
-        return (f"End to End Delay={_f(now - float(int(rec['start_s'])))}, Packet Size={self.data_size}, "
-                f"Current sim time ={_f(now)}, Pkt ID ={uid}, packetType =0"
+        return (f"End to End Delay={_f(now - start)}, Packet Size={size}, "
+                f"Current sim time ={_f(now)}, Pkt ID ={uid}, packetType ={ptype}"
                 f", Avg End to End Delay ={_f(float(avg_e2e))}, Avg Cost ={_f(float(avg_cost))}, "
                 f"Avg Underlay End to End Delay ={_f(0.0)}, Avg Underlay Cost ={_f(0.0)}"
                 f", Packets dropped ={lost}, Packets delivered ={arr}, Packets injected ={inj},"
                 f"Packets Buffered ={inj - (arr + lost)}"
                 f", Packets dropped Underlay ={ul}, Packets delivered Underlay={ua}, Packets injected Underlay={ui},"
                 f"Packets Buffered Underlay={ui - (ua + ul)}"
-                f",Signaling overhead ={_f(float(sig))}, Packet Lost={lost_ids}"
-                f", Source={src}, Destination={int(rec['dst'])}, node={v}")
+                f",Signaling overhead ={_f(float(sig))}")
+
+    def render(self, rec, cnt) -> str:
+        """DataPacketManager::getInfo for the notified data packet (22 tokens,
+        data-packet-manager.cc:230-248)."""
+        v = int(rec["node"])
+        now = int(rec["t_ns"]) / 1e9
+        lv = self.lost[v]
+        lost_ids = "".join("%u;" % u for u in reversed(lv))
+        lv.clear()
+        uid = int(rec["uid"])
+        return (self._stats(cnt, now, float(int(rec["start_s"])), self.data_size, uid, 0)
+                + f", Packet Lost={lost_ids}, Source={self.src.get(uid, v)}, Destination={int(rec['dst'])}, node={v}")
+
+    def render_ctrl(self, uid: int, cnt) -> str:
+        """SmallSignalingPacketManager::getInfo (small-signaling-packet-manager.cc:104-114): 20
+        tokens.  Token 3 (the echo's own ns-3 packet uid) carries the signalled uid."""
+        now = int(cnt["now_ns"]) / 1e9
+        return self._stats(cnt, now, 0.0, 30, uid, 2) + f", PacketIdSignaled={uid}, Arrived at final dest=1"
 
 
 class PrismaSession:
@@ -113,6 +124,7 @@ class PrismaSession:
         self.data_size = int(self.params["packet_size"]) + 30          # UDP 8 + IP 20 + PPP 2
         self._cv = threading.Condition()
         self.tracker = InfoTracker(self.N, self.data_size)
+        self._last_done = [False] * self.N
         self._pending = None                                             # (node, obs, done, info, dec)
         self._over = False
         self._closed = 0
@@ -128,20 +140,27 @@ class PrismaSession:
         prev = self._pending
         obs, mask, node = self.engine.step(a)
         cnt = self.engine.counters()[0]
-        if prev is not None:
+        if prev is not None and prev[4] is not None:
             self.tracker.applied(self.engine.records(0, prev[4], 1)[0])
         if int(mask.cpu()[0]) == 0:
             self._pending = None
             self._over = True
             return
-        d = int(cnt["dec_count"]) - 1
-        rec = self.engine.records(0, d, 1)[0]
-        assert int(rec["status"]) in (ST_PENDING, ST_DESTINATION)
         v = int(node.cpu()[0])
-        ob = [int(x) for x in obs.cpu().numpy()[0][:1 + self.deg[v]]]
-        self.tracker.notified(rec)
-        done = int(rec["status"]) == ST_DESTINATION
-        self._pending = (v, ob, done, self.tracker.render(rec, cnt), d)
+        row = obs.cpu().numpy()[0]
+        if int(row[0]) == 1000:
+            # small-signalling (--train) notification: obs [1000]; GetGameOver reports the
+            # node's last data notification (packet-routing-gym.cc:143-148)
+            self._pending = (v, [1000], self._last_done[v], self.tracker.render_ctrl(int(row[1]), cnt), None)
+        else:
+            d = int(cnt["dec_count"]) - 1
+            rec = self.engine.records(0, d, 1)[0]
+            assert int(rec["status"]) in (ST_PENDING, ST_DESTINATION)
+            ob = [int(x) for x in row[:1 + self.deg[v]]]
+            self.tracker.notified(rec)
+            done = int(rec["status"]) == ST_DESTINATION
+            self._last_done[v] = done
+            self._pending = (v, ob, done, self.tracker.render(rec, cnt), d)
         self.log.append(self._pending[:4])
 
     # -- single-threaded driver (tests, notebooks) -----------------------------

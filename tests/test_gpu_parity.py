@@ -43,13 +43,14 @@ def run_table_both(oracle_mod, topo, params, R, H, table, launches=1, replicas=N
     return cnt
 
 
-@pytest.mark.parametrize("name,tm,lf,ping,seed", [
-    ("abilene", 0, 1.0, 1, 100), ("abilene", 0, 1.0, 0, 100), ("abilene", 2, 2.0, 1, 7),
-    ("abilene", 3, 0.5, 0, 12345), ("geant", 0, 1.0, 1, 100), ("geant", 1, 1.5, 0, 3),
+@pytest.mark.parametrize("name,tm,lf,ping,seed,train", [
+    ("abilene", 0, 1.0, 1, 100, 0), ("abilene", 0, 1.0, 0, 100, 0), ("abilene", 2, 2.0, 1, 7, 0),
+    ("abilene", 3, 0.5, 0, 12345, 0), ("geant", 0, 1.0, 1, 100, 0), ("geant", 1, 1.5, 0, 3, 0),
+    ("abilene", 0, 1.0, 1, 100, 1), ("abilene", 1, 2.0, 0, 9, 1), ("geant", 0, 1.0, 1, 11, 1),
 ])
-def test_table_policy_parity(oracle_mod, name, tm, lf, ping, seed):
+def test_table_policy_parity(oracle_mod, name, tm, lf, ping, seed, train):
     topo = Topology.example(name, tm, lf)
-    params = engine_params(topo, sim_time_s=15.0, ping_as_obs=ping, seed=seed, replica_base=5)
+    params = engine_params(topo, sim_time_s=15.0, ping_as_obs=ping, seed=seed, replica_base=5, train=train)
     run_table_both(oracle_mod, topo, params, 6, 2500, sp_next_hop_table(topo))
 
 
@@ -101,6 +102,42 @@ def test_external_policy_step_parity(oracle_mod):
         ref_obs = [orcs[r].step(int(acts[r])) for r in range(R)]
         obs, mask, node = eng.step(torch.from_numpy(acts).cuda())
     torch.cuda.synchronize()
+    cnt = eng.counters()
+    log = eng.log_tensor().cpu().numpy()
+    for r in range(R):
+        ref = orcs[r].records()
+        assert eng.records(r, 0, len(ref), log_host=log).tobytes() == ref.tobytes()
+        assert_counters_equal(cnt[r], orcs[r].counters(), r)
+    eng.close()
+
+
+def test_external_notify_train_parity(oracle_mod):
+    """notify_dest + train: destination and small-signalling notifications reach the caller."""
+    topo = Topology.example("abilene", 0, 1.5)
+    params = engine_params(topo, sim_time_s=3.0, ping_as_obs=1, notify_dest=1, train=1)
+    R = 4
+    eng = PrismaEngine(topo, params, R)
+    eng.reset(0)
+    orcs = [oracle_mod.OracleSim(topo, params, replica=r) for r in range(R)]
+    ref_obs = [o.step(-1) for o in orcs]
+    obs, mask, node = eng.step(None)
+    rng = np.random.default_rng(5)
+    n_ctrl = 0
+    for s in range(1500):
+        g, m, nd = obs.cpu().numpy(), mask.cpu().numpy(), node.cpu().numpy()
+        acts = np.zeros(R, dtype=np.int32)
+        for r in range(R):
+            assert (ref_obs[r] is None) == (m[r] == 0), (s, r)
+            if ref_obs[r] is None:
+                continue
+            assert np.array_equal(ref_obs[r], g[r]), (s, r, g[r], ref_obs[r])
+            assert nd[r] == orcs[r].pending_node()
+            n_ctrl += int(g[r][0] == 1000)
+            acts[r] = rng.integers(0, topo.degrees[nd[r]])
+        ref_obs = [orcs[r].step(int(acts[r])) if ref_obs[r] is not None else None for r in range(R)]
+        obs, mask, node = eng.step(torch.from_numpy(acts).cuda())
+    torch.cuda.synchronize()
+    assert n_ctrl > 0
     cnt = eng.counters()
     log = eng.log_tensor().cpu().numpy()
     for r in range(R):

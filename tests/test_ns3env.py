@@ -22,20 +22,25 @@ def oracle_stream(oracle_mod, topo, params, policy, n):
     """(node, obs, done, info) of the first n notifications of the oracle."""
     o = oracle_mod.OracleSim(topo, params)
     out = []
+    last_done = [False] * topo.n_nodes
     obs = o.step(-1)
     while obs is not None and len(out) < n:
-        rec = o.records()[-1]
-        v = int(rec["node"])
-        W = 1 + int(topo.degrees[v])
-        done = int(rec["status"]) == 3
-        out.append((v, [int(x) for x in obs[:W]], done, o.last_info()))
+        v = o.pending_node()
+        if int(obs[0]) == 1000:                                  # small-signalling (control) notification
+            out.append((v, [1000], last_done[v], o.last_info()))
+        else:
+            rec = o.records()[-1]
+            W = 1 + int(topo.degrees[v])
+            done = int(rec["status"]) == 3
+            last_done[v] = done
+            out.append((v, [int(x) for x in obs[:W]], done, o.last_info()))
         obs = o.step(policy(v, obs))
     return o, out
 
 
 def sp_policy(topo):
     table = sp_next_hop_table(topo)
-    return lambda v, obs: 0 if obs[0] == v else int(table[v, obs[0]])
+    return lambda v, obs: 0 if obs[0] in (v, 1000) else int(table[v, obs[0]])
 
 
 def test_info_renderer_matches_oracle(oracle_mod):
@@ -62,6 +67,22 @@ def test_info_renderer_matches_oracle(oracle_mod):
     assert lost_seen > 0 and dest_seen > 0
 
 
+def test_control_info_renderer_matches_oracle(oracle_mod):
+    topo = Topology.example("abilene")
+    params = engine_params(topo, sim_time_s=2.0, ping_as_obs=1, notify_dest=1, train=1)
+    o = oracle_mod.OracleSim(topo, params)
+    tr = InfoTracker(topo.n_nodes, 542)
+    pol = sp_policy(topo)
+    obs, n_ctrl = o.step(-1), 0
+    while obs is not None and n_ctrl < 300:
+        v = o.pending_node()
+        if int(obs[0]) == 1000:
+            assert tr.render_ctrl(int(obs[1]), o.counters()) == o.last_info()
+            n_ctrl += 1
+        obs = o.step(pol(v, obs))
+    assert n_ctrl == 300
+
+
 def test_notify_dest_does_not_change_the_trajectory(oracle_mod):
     topo = Topology.example("abilene")
     base = engine_params(topo, sim_time_s=3.0, ping_as_obs=0)
@@ -76,10 +97,11 @@ def test_notify_dest_does_not_change_the_trajectory(oracle_mod):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")
-def test_session_stream_matches_oracle(oracle_mod):
+@pytest.mark.parametrize("train", [0, 1])
+def test_session_stream_matches_oracle(oracle_mod, train):
     from prisma_amd.ns3env import PrismaSession
     topo = Topology.example("abilene", 0, 2.0)
-    kw = dict(sim_time_s=2.0, ping_as_obs=1)
+    kw = dict(sim_time_s=2.0, ping_as_obs=1, train=train)
     pol = sp_policy(topo)
     _, ref = oracle_stream(oracle_mod, topo, engine_params(topo, notify_dest=1, **kw), pol, 1500)
     s = PrismaSession(topo=topo, base_port=7000, **kw)

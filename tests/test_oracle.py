@@ -208,3 +208,56 @@ def test_info_string_contract(oracle_mod):
     assert int(vals[1]) == 542
     for v in vals[5:18]:
         float(v)
+
+
+def test_train_echo_known_answer(oracle_mod):
+    """--train: a data notification at a non-source node echoes a 30-B
+    small-signalling packet to the last hop; it arrives tx(30 B) + 1 ms later as a
+    control notification [1000] with a 20-token info string."""
+    adj = np.array([[0, 1], [1, 0]])
+    tm = np.array([[0, 2000], [0, 0]], dtype=object)         # one slow flow 0 -> 1
+    topo = Topology.from_matrices(adj, tm)
+    p = engine_params(topo, sim_time_s=3.0, ping_as_obs=0, train=1, notify_dest=1)
+    s = oracle_mod.OracleSim(topo, p)
+    obs = s.step(-1)
+    events = []
+    while obs is not None and len(events) < 40:
+        info = s.last_info()
+        t = float(info.split(",")[2].split("=")[-1])
+        events.append((int(obs[0]), t, info))
+        obs = s.step(0)
+    data0 = [e for e in events if e[0] == 1 and "node=0" in e[2]]           # decisions at the source
+    dest1 = [e for e in events if e[0] == 1 and "node=1" in e[2]]           # done at the destination
+    ctrl = [e for e in events if e[0] == 1000]
+    assert data0 and dest1 and len(ctrl) == len(dest1)
+    # echo leaves node 1 at the destination notification and reaches node 0 after 0.48 + 1 ms
+    for (_, t1, i1), (_, tc, ic) in zip(dest1, ctrl):
+        assert abs((tc - t1) - 0.00148) < 2e-6
+        tok = ic.split(",")
+        assert len(tok) == 20 and int(tok[4].split("=")[-1]) == 2 and int(tok[1].split("=")[-1]) == 30
+        assert tok[18].split("=")[-1] == i1.split(",")[3].split("=")[-1]     # PacketIdSignaled = data uid
+        assert tok[19].split("=")[-1] == "1"
+    # no echo for the source's own notification, and train=0 sends none
+    q = oracle_mod.OracleSim(topo, dict(p, train=0))
+    obs, n_ctrl = q.step(-1), 0
+    while obs is not None:
+        n_ctrl += int(obs[0]) == 1000
+        obs = q.step(0)
+    assert n_ctrl == 0
+
+
+def test_train_echo_changes_dynamics_and_counts(oracle_mod):
+    topo = Topology.example("abilene")
+    table = sp_next_hop_table(topo)
+    p0 = engine_params(topo, sim_time_s=5.0, ping_as_obs=1)
+    a = oracle_mod.OracleSim(topo, p0)
+    a.run_table(table, 10 ** 9)
+    b = oracle_mod.OracleSim(topo, dict(p0, train=1))
+    b.run_table(table, 10 ** 9)
+    ca, cb = a.counters(), b.counters()
+    rb = b.records()
+    relayed = int((rb["prev"] >= 0).sum())                  # notifications at non-source nodes (SP: no loops)
+    # every relayed notification echoes 28 signalling bytes unless the echo was dropped
+    extra = int(cb["bytes_signaling"]) - int(ca["bytes_signaling"])
+    assert extra > 0 and int(cb["seq"]) > int(ca["seq"])
+    assert relayed > 0
