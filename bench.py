@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--tm", type=int, default=0)
     p.add_argument("--load-factor", type=float, default=1.0)
     p.add_argument("--ping-as-obs", type=int, default=1)
+    p.add_argument("--policy", default="dq_routing", choices=["dq_routing", "dqn_buffer", "sp"],
+                   help="in-kernel policy: DQ-routing argmin table (BASELINE configs[1]), DQN-buffer MLP, SP table")
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-hops", type=int, default=8000000, help="oracle hops per host thread (cpu_baseline)")
     return p.parse_args()
@@ -131,18 +133,25 @@ def main():
     from prisma_amd.dist import gather_replica_stats, shard
     from prisma_amd.engine import PrismaEngine
     from prisma_amd.policies import StackedQNet
-    from prisma_amd.topology import Topology
+    from prisma_amd.topology import Topology, sp_next_hop_table
 
     topo = Topology.example(args.topology, args.tm, args.load_factor)
     base, R = shard(args.replicas * world, rank, world)
     params = engine_params(topo, sim_time_s=60.0, ping_as_obs=args.ping_as_obs, auto_reset=1,
                            replica_base=base, seed=100)
     eng = PrismaEngine(topo, params, R, device=local)
-    agent = StackedQNet(topo, "routing", seed=1234, device=dev)
+    if args.policy == "dqn_buffer":
+        agent = StackedQNet(topo, "buffer", seed=1234, device=dev)
+        policy = agent.pack                       # packed weights, decided in-kernel per hop
+    elif args.policy == "sp":
+        sp = torch.from_numpy(sp_next_hop_table(topo)).to(dev)
+        policy = lambda: sp
+    else:
+        agent = StackedQNet(topo, "routing", seed=1234, device=dev)
+        policy = agent.argmin_table               # policy forward for every (node, dst)
 
     def step():
-        table = agent.argmin_table()              # policy forward for every (node, dst)
-        eng.run(table, args.hops)
+        eng.run(policy(), args.hops)
 
     eng.reset(0)
     for _ in range(args.warmup):
@@ -156,11 +165,11 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        table = agent.argmin_table()
+        pol = policy()
         e0 = torch.cuda.Event(enable_timing=True)
         e1 = torch.cuda.Event(enable_timing=True)
         e0.record(stream)
-        eng.run(table, args.hops)
+        eng.run(pol, args.hops)
         e1.record(stream)
         evs.append((e0, e1))
     torch.cuda.synchronize()
@@ -205,13 +214,13 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": f"synthetic (Poisson traffic from the shipped {topo.name} TM{args.tm} x load_factor "
-                    f"{args.load_factor}; random-init DQ-routing weights)",
+                    f"{args.load_factor}; {'random-init ' + args.policy + ' weights' if args.policy != 'sp' else 'SP table'})",
             "config": {
-                "workload": f"{args.topology} tm{args.tm} lf{args.load_factor} dq_routing greedy, "
+                "workload": f"{args.topology} tm{args.tm} lf{args.load_factor} {args.policy} greedy, "
                             f"{args.replicas} replicas/GPU x {args.hops} hops/step, pingAsObs={args.ping_as_obs}, "
                             f"simTime 60 s auto-reset",
                 "topology": args.topology, "replicas_per_gpu": args.replicas, "hops_per_step": args.hops,
-                "policy": "dq_routing", "parallelism": f"replica-sharded x{world}",
+                "policy": args.policy, "parallelism": f"replica-sharded x{world}",
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -223,9 +232,9 @@ def main():
             "errors": errors,
             "episodes_completed": stats["episodes_completed"],
         }
-        if args.cpu_baseline and world == 1:
+        if args.cpu_baseline and world == 1 and args.policy != "dqn_buffer":
             result["cpu_baseline"] = cpu_baseline(topo, dict(params, auto_reset=0),
-                                                  agent.argmin_table().cpu().numpy(), args.cpu_hops)
+                                                  policy().cpu().numpy(), args.cpu_hops)
         print(json.dumps(result), flush=True)
     eng.close()
     if world > 1:

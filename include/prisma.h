@@ -60,6 +60,11 @@ extern "C" {
 
 /* policy modes for prisma_run (fused decision) */
 #define PRISMA_POLICY_TABLE    1   /* action = table[node * n_nodes + dst] */
+#define PRISMA_POLICY_DQN_BUFFER 2 /* in-kernel DQN_buffer_model (models.py:258-306)
+                                      over packed fp32 weights, D = max_deg:
+                                      W1[N][N][32] b1[N][32] Wb[N][D][32] bb[N][32]
+                                      W2[N][64][64] b2[N][64] W3[N][64][64] b3[N][64]
+                                      W4[N][64][D] b4[N][D]; x @ W convention     */
 
 /* per-decision status (prisma_record_t.status) */
 #define PRISMA_ST_PENDING      0   /* waiting for an action (prisma_step)  */
@@ -223,11 +228,13 @@ int prisma_step(prisma_env_t* env, const int32_t* actions, int32_t* obs_out,
                 uint8_t* mask_out, int32_t* node_out, void* stream);
 
 /* Fused policy: advance every replica by up to max_hops hops, deciding
- * in-kernel with `table` (device uint8 [n_nodes][n_nodes] action table).
+ * in-kernel: PRISMA_POLICY_TABLE with `policy_data` = device uint8
+ * [n_nodes][n_nodes] action table (SP, DQ-routing argmin), or
+ * PRISMA_POLICY_DQN_BUFFER with `policy_data` = device packed fp32 weights.
  * A replica stops early at the end of its episode; with params.auto_reset
  * it starts the next episode before the call returns (one launch never
  * crosses an episode boundary). */
-int prisma_run(prisma_env_t* env, int32_t policy, const uint8_t* table,
+int prisma_run(prisma_env_t* env, int32_t policy, const void* policy_data,
                int32_t max_hops, void* stream);
 
 /* Copy per-replica counters (n_replicas entries) to host memory.

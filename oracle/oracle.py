@@ -52,6 +52,12 @@ def lib():
         L.or_step.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
         L.or_run_table.restype = C.c_int64
         L.or_run_table.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.or_run_mlp.restype = C.c_int64
+        L.or_run_mlp.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        L.or_mlp_action.restype = C.c_int32
+        L.or_mlp_action.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+        L.or_det_expm1.restype = C.c_double
+        L.or_det_expm1.argtypes = [C.c_double]
         L.or_pending_node.restype = C.c_int32
         L.or_pending_node.argtypes = [C.c_void_p]
         L.or_record_count.restype = C.c_int64
@@ -77,6 +83,10 @@ def lib():
         L.or_py_micros.argtypes = [C.c_int64]
         _lib = L
     return _lib
+
+
+def det_expm1(x: float) -> float:
+    return float(lib().or_det_expm1(float(x)))
 
 
 def philox(ctr, key):
@@ -173,6 +183,15 @@ class OracleSim:
         out = np.zeros((n, 4), dtype=np.int64)
         lib().or_copy_trace(self.h, 0, n, out.ctypes.data)
         return out
+
+    def run_mlp(self, weights: np.ndarray, max_hops: int) -> int:
+        w = np.ascontiguousarray(weights, dtype=np.float32)
+        return int(lib().or_run_mlp(self.h, w.ctypes.data, int(max_hops)))
+
+    def mlp_action(self, weights: np.ndarray, node: int, obs) -> int:
+        w = np.ascontiguousarray(weights, dtype=np.float32)
+        o = np.ascontiguousarray(obs, dtype=np.uint32)
+        return int(lib().or_mlp_action(self.h, w.ctypes.data, int(node), o.ctypes.data))
 
     def pending_node(self) -> int:
         return int(lib().or_pending_node(self.h))

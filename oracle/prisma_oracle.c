@@ -826,6 +826,100 @@ int64_t or_run_table(or_sim_t* s, const uint8_t* table, int64_t max_hops) {
     return (int64_t)(s->cnt.hops - h0);
 }
 
+/* ------------------------------------------------------------------ */
+/* DQN_buffer_model (models.py:258-306) restated in fp32 with a fixed    */
+/* operation order: the checker for the in-kernel MLP.    */
+/* ------------------------------------------------------------------ */
+double or_det_expm1(double x) {                 /* x <= 0; + - * / only */
+    if (x < -60.0) return -1.0;
+    double t = x * 1.4426950408889634 + 0.5;
+    int64_t ki = (int64_t)t;
+    if ((double)ki > t) ki -= 1;
+    double k = (double)ki;
+    double r = (x - k * 6.93147180369123816490e-01) - k * 1.90821492927058770002e-10;
+    static const double inv_fact[14] = { 1.0 / 6227020800.0, 1.0 / 479001600.0, 1.0 / 39916800.0, 1.0 / 3628800.0,
+                                         1.0 / 362880.0, 1.0 / 40320.0, 1.0 / 5040.0, 1.0 / 720.0, 1.0 / 120.0,
+                                         1.0 / 24.0, 1.0 / 6.0, 0.5, 1.0, 0.0 };
+    double p = r * (1.0 / 87178291200.0);
+    for (int i = 0; i < 13; ++i) p = (p + inv_fact[i]) * r;
+    if (ki == 0) return p;
+    uint64_t bits = (uint64_t)(1023 + ki) << 52;
+    double scale;
+    memcpy(&scale, &bits, 8);
+    return scale * (p + 1.0) - 1.0;
+}
+
+static float elu_f(float x) { return x > 0.0f ? x : (float)or_det_expm1((double)x); }
+
+/* Packed weights (float): W1[N][N][32] b1[N][32] Wb[N][D][32] bb[N][32] W2[N][64][64] b2[N][64]
+ * W3[N][64][64] b3[N][64] W4[N][64][D] b4[N][D], D = max_deg (prisma_amd.policies.StackedQNet.pack). */
+static int mlp_action(const or_sim_t* s, const float* w, int v, const uint32_t* obs) {
+    const int N = s->N, D = s->c.max_deg;
+    const float* W1 = w;
+    const float* b1 = W1 + (size_t)N * N * 32;
+    const float* Wb = b1 + (size_t)N * 32;
+    const float* bb = Wb + (size_t)N * D * 32;
+    const float* W2 = bb + (size_t)N * 32;
+    const float* b2 = W2 + (size_t)N * 64 * 64;
+    const float* W3 = b2 + (size_t)N * 64;
+    const float* b3 = W3 + (size_t)N * 64 * 64;
+    const float* W4 = b3 + (size_t)N * 64;
+    const float* b4 = W4 + (size_t)N * 64 * D;
+    int deg = s->c.row_ptr[v + 1] - s->c.row_ptr[v];
+    int dst = (int)obs[0];
+    float x[128], xn[128], h[64], h2[64];
+    float sum = 0.0f, var = 0.0f;
+    for (int k = 0; k < deg; ++k) { x[k] = (float)obs[1 + k]; sum = sum + x[k]; }
+    float mean = sum / (float)deg;
+    for (int k = 0; k < deg; ++k) { float d = x[k] - mean; var = var + d * d; }
+    var = var / (float)deg;
+    float den = sqrtf(var + 1e-3f);                         /* LayerNormalization, epsilon 1e-3 */
+    for (int k = 0; k < deg; ++k) xn[k] = (x[k] - mean) / den;
+    for (int j = 0; j < 32; ++j) h[j] = elu_f(W1[((size_t)v * N + dst) * 32 + j] + b1[v * 32 + j]);
+    for (int j = 0; j < 32; ++j) {
+        float acc = 0.0f;
+        for (int k = 0; k < deg; ++k) acc = fmaf(xn[k], Wb[((size_t)v * D + k) * 32 + j], acc);
+        h[32 + j] = elu_f(acc + bb[v * 32 + j]);
+    }
+    for (int j = 0; j < 64; ++j) {
+        float acc = 0.0f;
+        for (int i = 0; i < 64; ++i) acc = fmaf(h[i], W2[((size_t)v * 64 + i) * 64 + j], acc);
+        h2[j] = elu_f(acc + b2[v * 64 + j]);
+    }
+    for (int j = 0; j < 64; ++j) {
+        float acc = 0.0f;
+        for (int i = 0; i < 64; ++i) acc = fmaf(h2[i], W3[((size_t)v * 64 + i) * 64 + j], acc);
+        h[j] = elu_f(acc + b3[v * 64 + j]);
+    }
+    int best = 0;
+    float bq = 0.0f;
+    for (int a = 0; a < deg; ++a) {
+        float acc = 0.0f;
+        for (int i = 0; i < 64; ++i) acc = fmaf(h[i], W4[((size_t)v * 64 + i) * D + a], acc);
+        float q = elu_f(acc + b4[v * D + a]);
+        if (a == 0 || q < bq) { bq = q; best = a; }          /* tf.argmin: first minimum */
+    }
+    return best;
+}
+
+int64_t or_run_mlp(or_sim_t* s, const float* weights, int64_t max_hops) {
+    uint64_t h0 = s->cnt.hops;
+    while ((int64_t)(s->cnt.hops - h0) < max_hops) {
+        if (s->pend) {
+            rec_head_t* r = rec_at(s, s->pend_rec);
+            const uint32_t* o = (const uint32_t*)((unsigned char*)r + sizeof(rec_head_t));
+            finish_data_decision(s, mlp_action(s, weights, r->node, o));
+            continue;
+        }
+        if (!run_until_decision(s)) break;
+    }
+    return (int64_t)(s->cnt.hops - h0);
+}
+
+int32_t or_mlp_action(or_sim_t* s, const float* weights, int32_t v, const uint32_t* obs) {
+    return mlp_action(s, weights, v, obs);
+}
+
 int64_t or_record_count(const or_sim_t* s) { return s->rec_n; }
 int32_t or_pending_node(const or_sim_t* s) { return s->pend ? s->pend_node : -1; }
 int32_t or_obs_width(const or_sim_t* s) { return s->W; }

@@ -97,7 +97,7 @@ struct Layout {
     int32_t N, E, L, F, W, max_deg, WCAP, MA;
     uint32_t topo_bytes, state_bytes, lds_bytes, table_bytes;
     // state image (LDS offset 0) and the action table (LDS offset lds_state_bytes)
-    uint32_t s_hdr, s_cnt, s_obs, s_wt, s_wseq, s_ring, s_win, s_pbd;
+    uint32_t s_hdr, s_cnt, s_obs, s_wt, s_wseq, s_ring, s_win, s_pbd, s_mlp;
     uint32_t lds_state_bytes;    // LDS part of the image (bytes [0, lds_state_bytes))
     uint32_t s_regs;             // register part: 4 x [64*FS] + 20 x [64*LS] u32 arrays
     uint32_t PBK;                // ping-back delay slots per tunnel (power of two)

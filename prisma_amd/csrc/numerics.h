@@ -51,6 +51,38 @@ __host__ __device__ inline double det_log(double x) {
     return de * 6.93147180369123816490e-01 + (de * 1.90821492927058770002e-10 + logm);
 }
 
+// expm1(x) for x <= 0 in double with + - * / only: x = k ln2 + r, |r| <= ln2/2,
+// expm1(r) by its Taylor series, then 2^k (1 + expm1(r)) - 1.  Used by the
+// in-kernel DQN MLP's ELU; identical bits on host and device.
+__host__ __device__ inline double det_expm1(double x) {
+    if (x < -60.0) return -1.0;
+    double t = x * 1.4426950408889634 + 0.5;
+    int64_t ki = (int64_t)t;                       // truncation toward zero ...
+    if ((double)ki > t) ki -= 1;                   // ... to floor
+    double k = (double)ki;
+    double r = (x - k * 6.93147180369123816490e-01) - k * 1.90821492927058770002e-10;
+    double p = r * (1.0 / 87178291200.0);          // 1/14!
+    p = (p + 1.0 / 6227020800.0) * r;
+    p = (p + 1.0 / 479001600.0) * r;
+    p = (p + 1.0 / 39916800.0) * r;
+    p = (p + 1.0 / 3628800.0) * r;
+    p = (p + 1.0 / 362880.0) * r;
+    p = (p + 1.0 / 40320.0) * r;
+    p = (p + 1.0 / 5040.0) * r;
+    p = (p + 1.0 / 720.0) * r;
+    p = (p + 1.0 / 120.0) * r;
+    p = (p + 1.0 / 24.0) * r;
+    p = (p + 1.0 / 6.0) * r;
+    p = (p + 0.5) * r;
+    p = (p + 1.0) * r;                             // expm1(r)
+    if (ki == 0) return p;
+    double scale = __builtin_bit_cast(double, (uint64_t)(1023 + ki) << 52);
+    return scale * (p + 1.0) - 1.0;
+}
+
+// Keras ELU (alpha 1): x > 0 ? x : expm1(x), rounded to float
+__host__ __device__ inline float det_elu(float x) { return x > 0.0f ? x : (float)det_expm1((double)x); }
+
 // ns-3 Seconds(double) -> int64 ns (round to nearest)
 __host__ __device__ inline int64_t sec_to_ns(double s) { return (int64_t)(s * 1e9 + 0.5); }
 // ns-3 Time::GetSeconds()

@@ -68,6 +68,7 @@ struct KParams {
     uint8_t* mask_out;           // [R] or null
     int32_t* node_out;           // [R] or null
     const uint8_t* table;        // [N][N] or null
+    const float* mlp;            // packed DQN-buffer weights or null (mode 4)
     int32_t R;
     int32_t max_hops;
     uint32_t episode;            // reset kernel only
@@ -215,6 +216,7 @@ struct LV {
     __device__ __forceinline__ uint32_t s_ring() const { return (uint32_t)u(offsetof(Layout, s_ring) / 4); }
     __device__ __forceinline__ uint32_t s_win() const { return (uint32_t)u(offsetof(Layout, s_win) / 4); }
     __device__ __forceinline__ uint32_t s_pbd() const { return (uint32_t)u(offsetof(Layout, s_pbd) / 4); }
+    __device__ __forceinline__ uint32_t s_mlp() const { return (uint32_t)u(offsetof(Layout, s_mlp) / 4); }
     __device__ __forceinline__ uint32_t lds_state_bytes() const { return (uint32_t)u(offsetof(Layout, lds_state_bytes) / 4); }
     __device__ __forceinline__ uint32_t s_regs() const { return (uint32_t)u(offsetof(Layout, s_regs) / 4); }
     __device__ __forceinline__ uint32_t PBK() const { return (uint32_t)u(offsetof(Layout, PBK) / 4); }
@@ -260,6 +262,8 @@ struct Sim {
     float* pbd;                             // ping-back delays [E][PBK]
     const CAS TopoImage* T;                 // topology (scalar loads at fixed offsets)
     const uint8_t* table;
+    const float* mlp;                       // DQN-buffer weights (HBM) or null
+    float* hbuf;                            // 64 floats of LDS: a layer's activations
     unsigned char* logrep;
     uint32_t gid;
     int lane;
@@ -282,6 +286,8 @@ __device__ inline void sim_bind(Sim& S, const LV& L, unsigned char* lds, const u
     S.pbd = (float*)(lds + L.s_pbd());
     S.T = (const CAS TopoImage*)topo;
     S.table = (const uint8_t*)(lds + L.lds_state_bytes());
+    S.hbuf = (float*)(lds + L.s_mlp());
+    S.mlp = nullptr;
     S.logrep = logrep;
     S.gid = gid;
     S.lane = lane;
@@ -697,6 +703,81 @@ __device__ __forceinline__ void on_flow(const Sim& S, Regs<FS, LS>& R, Hot& H, u
     flow_next(S, R, H, f, draw);                                    // StartSending / ScheduleNextTx
 }
 
+// ---- in-kernel DQN_buffer_model (models.py:258-306; fixed fp32 operation order,
+// DESIGN.md §2, restated by the oracle's mlp_action): lane j computes unit j of
+// each layer, activations are broadcast through 64 floats of LDS, weights are
+// read per lane from HBM (L2-resident, shared by every replica).
+__device__ __forceinline__ float hb_ld(const Sim& S, int i) { return S.hbuf[i]; }
+
+__device__ __forceinline__ float mlp_dense64(const Sim& S, const float* __restrict__ W, int lane, int stride) {
+    float acc = 0.0f;
+#pragma unroll 16
+    for (int i = 0; i < 64; ++i) acc = __builtin_fmaf(hb_ld(S, i), W[i * stride + lane], acc);
+    return acc;
+}
+
+__device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t dst, uint32_t obs_reg) {
+    const LV& L = S.lv;
+    const int lane = S.lane;
+    const int N = L.N(), D = L.max_deg();
+    const float* __restrict__ W1 = S.mlp;
+    const float* __restrict__ b1 = W1 + N * N * 32;
+    const float* __restrict__ Wb = b1 + N * 32;
+    const float* __restrict__ bb = Wb + N * D * 32;
+    const float* __restrict__ W2 = bb + N * 32;
+    const float* __restrict__ b2 = W2 + N * 64 * 64;
+    const float* __restrict__ W3 = b2 + N * 64;
+    const float* __restrict__ b3 = W3 + N * 64 * 64;
+    const float* __restrict__ W4 = b3 + N * 64;
+    const float* __restrict__ b4 = W4 + N * 64 * D;
+    const int deg = S.T->rowptr[v + 1] - S.T->rowptr[v];
+    // LayerNormalization of the deg buffer values (population variance, epsilon 1e-3)
+    float sum = 0.0f;
+    for (int k = 0; k < deg; ++k) sum = __fadd_rn(sum, (float)rdl(obs_reg, (uint32_t)(k + 1)));
+    const float mean = __fdiv_rn(sum, (float)deg);
+    float var = 0.0f;
+    for (int k = 0; k < deg; ++k) {
+        const float d = __fsub_rn((float)rdl(obs_reg, (uint32_t)(k + 1)), mean);
+        var = __fadd_rn(var, __fmul_rn(d, d));
+    }
+    var = __fdiv_rn(var, (float)deg);
+    const float den = __fsqrt_rn(__fadd_rn(var, 1e-3f));
+    // layer 1: one-hot(dst) branch in lanes 0-31, buffers branch in lanes 32-63
+    float h;
+    if (lane < 32) {
+        h = det_elu(__fadd_rn(W1[((int)v * N + (int)dst) * 32 + lane], b1[(int)v * 32 + lane]));
+    } else {
+        const int j = lane - 32;
+        float acc = 0.0f;
+        for (int k = 0; k < deg; ++k) {
+            const float xn = __fdiv_rn(__fsub_rn((float)rdl(obs_reg, (uint32_t)(k + 1)), mean), den);
+            acc = __builtin_fmaf(xn, Wb[((int)v * D + k) * 32 + j], acc);
+        }
+        h = det_elu(__fadd_rn(acc, bb[(int)v * 32 + j]));
+    }
+    S.hbuf[lane] = h;
+    __builtin_amdgcn_wave_barrier();
+    h = det_elu(__fadd_rn(mlp_dense64(S, W2 + (int)v * 64 * 64, lane, 64), b2[(int)v * 64 + lane]));
+    __builtin_amdgcn_wave_barrier();
+    S.hbuf[lane] = h;
+    __builtin_amdgcn_wave_barrier();
+    h = det_elu(__fadd_rn(mlp_dense64(S, W3 + (int)v * 64 * 64, lane, 64), b3[(int)v * 64 + lane]));
+    __builtin_amdgcn_wave_barrier();
+    S.hbuf[lane] = h;
+    __builtin_amdgcn_wave_barrier();
+    float q = 0.0f;
+    if (lane < deg) q = det_elu(__fadd_rn(mlp_dense64(S, W4 + (int)v * 64 * D, lane, D), b4[(int)v * D + lane]));
+    __builtin_amdgcn_wave_barrier();
+    // tf.argmin: first minimum (learner.py:145)
+    int best = 0;
+    float bq = __uint_as_float(rdl(__float_as_uint(q), 0));
+    for (int a = 1; a < deg; ++a) {
+        const float qa = __uint_as_float(rdl(__float_as_uint(q), (uint32_t)a));
+        if (qa < bq) { bq = qa; best = a; }
+    }
+    return best;
+}
+
 // the head packet leaves the wire of link l (arrival at the far end)
 template <int FS, int LS>
 __device__ __forceinline__ void wire_pop(const Sim& S, Regs<FS, LS>& R, const Hot& H, uint32_t l, LinkV& k) {
@@ -1109,7 +1190,9 @@ template <int FS, int LS> struct StepOcc {
     static constexpr int waves = (FS <= 2 && LS == 1) ? 4 : (LS <= 2 ? 2 : 1);
 };
 
-template <int FS, int LS>
+// MLP: the in-kernel DQN-buffer policy is compiled in (mode 4 only); the table /
+// external instances carry none of its code or registers.
+template <int FS, int LS, bool MLP>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(StepOcc<FS, LS>::waves)))
 prisma_step_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -1123,7 +1206,9 @@ prisma_step_kernel_t(KParams P) {
     Sim S;
     sim_bind(S, lv, lds, P.topo, P.log + (size_t)r * LC.log_cap * LC.rec_bytes, LC.replica_base + (uint32_t)r, lane);
     const LV& L = S.lv;
-    const bool table_mode = (P.mode == 2);
+    const bool mlp_mode = MLP;
+    const bool table_mode = (P.mode == 2) || mlp_mode;            // fused in-kernel policy
+    S.mlp = P.mlp;
     const uint32_t max_hops = (uint32_t)P.max_hops;
     const uint32_t NN = (uint32_t)L.N();
     Hot H;
@@ -1134,7 +1219,9 @@ prisma_step_kernel_t(KParams P) {
     if (H.pend && !H.over) {
         if (table_mode) {
             uint32_t pn = u_ld32(&S.h->pend_node), pd = u_ld32(&S.h->pend_ent[1]);
-            H.hops_launch += finish_pending(S, R, H, (int)rfl((uint32_t)S.table[pn * NN + pd]));
+            const int a = mlp_mode ? mlp_action(S, pn, pd, (lane < L.W()) ? S.obs[lane] : 0u)
+                                   : (int)rfl((uint32_t)S.table[pn * NN + pd]);
+            H.hops_launch += finish_pending(S, R, H, a);
         } else if (P.actions) {
             finish_pending(S, R, H, (int)rfl((uint32_t)P.actions[r]));
         } else {
@@ -1180,8 +1267,9 @@ prisma_step_kernel_t(KParams P) {
             TM_MARK(1);
             if (need) {
                 if (table_mode) {
-                    int a = (int)S.table[D.v * NN + D.dst];
-                    apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, (int)rfl((uint32_t)a), true,
+                    const int a = mlp_mode ? mlp_action(S, D.v, D.dst, D.obs)
+                                           : (int)rfl((uint32_t)S.table[D.v * NN + D.dst]);
+                    apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, a, true,
                                    D.reward, D.prev, D.obs,
                                    (D.flags & PEND_ECHO) ? (uint32_t)S.T->lrev[id] : kNoLink);
                     H.hops_launch++;
@@ -1234,12 +1322,15 @@ prisma_step_kernel_t(KParams P) {
 // instantiations: flow slots FS in {1,2,4,8} (F <= 512), link slots LS in {1,2,4} (L <= 256)
 typedef void (*kernel_fn)(KParams);
 template <int FS, int LS> struct KPair {
-    static const void* step() { return (const void*)prisma_step_kernel_t<FS, LS>; }
+    static const void* step() { return (const void*)prisma_step_kernel_t<FS, LS, false>; }
+    static const void* step_mlp() { return (const void*)prisma_step_kernel_t<FS, LS, true>; }
     static const void* reset() { return (const void*)prisma_reset_kernel_t<FS, LS>; }
 };
 
-static const void* pick_kernel(int fs, int ls, bool reset) {
-#define PK(F_, L_) if (fs == F_ && ls == L_) return reset ? KPair<F_, L_>::reset() : KPair<F_, L_>::step();
+// which: 0 step (table / external), 1 reset, 2 step with the DQN-buffer policy
+static const void* pick_kernel(int fs, int ls, int which) {
+#define PK(F_, L_) if (fs == F_ && ls == L_) \
+    return which == 1 ? KPair<F_, L_>::reset() : (which == 2 ? KPair<F_, L_>::step_mlp() : KPair<F_, L_>::step());
     PK(1, 1) PK(1, 2) PK(1, 4) PK(2, 1) PK(2, 2) PK(2, 4) PK(4, 1) PK(4, 2) PK(4, 4) PK(8, 1) PK(8, 2) PK(8, 4)
 #undef PK
     return nullptr;
@@ -1276,6 +1367,7 @@ struct prisma_env {
     prisma_counters_t* d_cnt = nullptr;
     Layout* d_lay = nullptr;
     const void* k_step = nullptr;
+    const void* k_step_mlp = nullptr;
     const void* k_reset = nullptr;
     bool reset_done = false;
 };
@@ -1433,7 +1525,8 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 20u * 64u * (uint32_t)ls));
     L.state_bytes = o;
     L.lds_bytes = L.lds_state_bytes + align16(L.table_bytes);
-    if (L.lds_bytes > 160u * 1024u)
+    L.s_mlp = L.lds_bytes;                          // + 256 B of DQN-buffer activations (MLP launches only)
+    if (L.lds_bytes + 256u > 160u * 1024u)
         return set_err(PRISMA_ERR_CONFIG, "replica state exceeds the 160 KiB LDS of a gfx950 CU");
 
     L.t_end = sec_to_ns(P->sim_time_s);
@@ -1488,8 +1581,10 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
         prisma_destroy(e);
         return set_err(PRISMA_ERR_DEVICE, "device initialisation failed");
     }
-    e->k_step = pick_kernel(L.FS, L.LS, false);
-    e->k_reset = pick_kernel(L.FS, L.LS, true);
+    e->k_step = pick_kernel(L.FS, L.LS, 0);
+    e->k_reset = pick_kernel(L.FS, L.LS, 1);
+    e->k_step_mlp = pick_kernel(L.FS, L.LS, 2);
+    (void)hipFuncSetAttribute(e->k_step_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes + 256);
     (void)hipFuncSetAttribute(e->k_step, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
     (void)hipFuncSetAttribute(e->k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
     *out = e;
@@ -1511,7 +1606,8 @@ static KParams base_params(prisma_env_t* e) {
 static int launch(prisma_env_t* e, const void* kern, KParams P, void* stream) {
     (void)hipSetDevice(e->device);
     void* args[] = { &P };
-    hipError_t err = hipLaunchKernel(kern, dim3((unsigned)e->R), dim3(kWave), args, e->lay.lds_bytes, (hipStream_t)stream);
+    const size_t lds = e->lay.lds_bytes + (kern == e->k_step_mlp ? 256u : 0u);
+    hipError_t err = hipLaunchKernel(kern, dim3((unsigned)e->R), dim3(kWave), args, lds, (hipStream_t)stream);
     if (err == hipSuccess) err = hipGetLastError();
     if (err != hipSuccess) return set_err(PRISMA_ERR_LAUNCH, std::string("kernel launch failed: ") + hipGetErrorString(err));
     return PRISMA_OK;
@@ -1550,16 +1646,23 @@ extern "C" int prisma_step(prisma_env_t* e, const int32_t* actions, int32_t* obs
     return rc ? rc : auto_reset(e, stream);
 }
 
-extern "C" int prisma_run(prisma_env_t* e, int32_t policy, const uint8_t* table, int32_t max_hops, void* stream) {
+extern "C" int prisma_run(prisma_env_t* e, int32_t policy, const void* policy_data, int32_t max_hops, void* stream) {
     if (!e) return set_err(PRISMA_ERR_ARG, "null env");
     if (!e->reset_done) return set_err(PRISMA_ERR_STATE, "prisma_reset must be called first");
-    if (policy != PRISMA_POLICY_TABLE || !table) return set_err(PRISMA_ERR_ARG, "policy must be PRISMA_POLICY_TABLE with a device table");
+    if ((policy != PRISMA_POLICY_TABLE && policy != PRISMA_POLICY_DQN_BUFFER) || !policy_data)
+        return set_err(PRISMA_ERR_ARG, "policy must be PRISMA_POLICY_TABLE (uint8 table) or "
+                                       "PRISMA_POLICY_DQN_BUFFER (fp32 weights), with device data");
     if (max_hops < 1) return set_err(PRISMA_ERR_ARG, "max_hops must be >= 1");
     KParams P = base_params(e);
-    P.mode = 2;
-    P.table = table;
+    if (policy == PRISMA_POLICY_TABLE) {
+        P.mode = 2;
+        P.table = (const uint8_t*)policy_data;
+    } else {
+        P.mode = 4;
+        P.mlp = (const float*)policy_data;
+    }
     P.max_hops = max_hops;
-    int rc = launch(e, e->k_step, P, stream);
+    int rc = launch(e, P.mode == 4 ? e->k_step_mlp : e->k_step, P, stream);
     return rc ? rc : auto_reset(e, stream);
 }
 

@@ -18,6 +18,12 @@ from .topology import Topology
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprisma_amd.so")
 
 PRISMA_POLICY_TABLE = 1
+PRISMA_POLICY_DQN_BUFFER = 2
+
+
+def dqn_buffer_floats(n: int, d: int) -> int:
+    """Length of the packed DQN-buffer weights (include/prisma.h PRISMA_POLICY_DQN_BUFFER)."""
+    return n * n * 32 + n * 32 + n * d * 32 + n * 32 + 2 * (n * 64 * 64 + n * 64) + n * 64 * d + n * d
 
 
 class PrismaError(RuntimeError):
@@ -207,14 +213,23 @@ class PrismaEngine:
                                 _stream_handle(stream)))
         return self.obs, self.mask, self.node
 
-    def run(self, table, max_hops: int, stream=None):
-        """Fused policy: every replica executes up to max_hops hops with an [N, N] action table."""
+    def run(self, policy, max_hops: int, stream=None):
+        """Fused in-kernel policy: every replica executes up to max_hops hops.
+
+        policy: a device uint8 [N, N] action table (SP, DQ-routing argmin), or the device fp32
+        packed DQN-buffer weights of StackedQNet(kind="buffer").pack()."""
         import torch
-        n = self.topo.n_nodes
-        if table.dtype != torch.uint8 or tuple(table.shape) != (n, n) or not table.is_cuda:
-            raise PrismaError("table must be a device uint8 tensor of shape [n_nodes, n_nodes]")
-        _check(_lib.prisma_run(self.h, PRISMA_POLICY_TABLE, table.contiguous().data_ptr(), int(max_hops),
-                               _stream_handle(stream)))
+        n, d = self.topo.n_nodes, self.topo.max_deg
+        if not policy.is_cuda:
+            raise PrismaError("policy data must live on the device")
+        if policy.dtype == torch.uint8 and tuple(policy.shape) == (n, n):
+            kind = PRISMA_POLICY_TABLE
+        elif policy.dtype == torch.float32 and policy.dim() == 1 and policy.numel() == dqn_buffer_floats(n, d):
+            kind = PRISMA_POLICY_DQN_BUFFER
+        else:
+            raise PrismaError("policy must be a uint8 [n_nodes, n_nodes] table or packed fp32 DQN-buffer weights")
+        self._policy_keep = policy.contiguous()
+        _check(_lib.prisma_run(self.h, kind, self._policy_keep.data_ptr(), int(max_hops), _stream_handle(stream)))
 
     # -- outputs ----------------------------------------------------------
     def counters(self, stream=None) -> np.ndarray:

@@ -116,6 +116,16 @@ class StackedQNet(torch.nn.Module):
         return torch.argmin(self.q_values(obs, node), dim=1).to(torch.int32)
 
     @torch.no_grad()
+    def pack(self) -> torch.Tensor:
+        """Flat fp32 weights for the in-kernel DQN-buffer policy (PRISMA_POLICY_DQN_BUFFER):
+        W1[N][N][32] b1[N][32] Wb[N][D][32] bb[N][32] W2[N][64][64] b2[N][64] W3[N][64][64]
+        b3[N][64] W4[N][64][D] b4[N][D] (include/prisma.h)."""
+        if self.kind != "buffer":
+            raise ValueError("pack() is the DQN-buffer layout (kind='buffer')")
+        parts = [self.W1, self.b1, self.Wb, self.bb, self.W2, self.b2, self.W3, self.b3, self.W4, self.b4]
+        return torch.cat([p.detach().to(torch.float32).contiguous().flatten() for p in parts])
+
+    @torch.no_grad()
     def argmin_table(self) -> torch.Tensor:
         """[N, N] uint8 action table (valid for kind='routing': Q depends on (node, dst) only)."""
         if self.kind != "routing":

@@ -263,3 +263,39 @@ def test_vec_env_transitions_match_oracle_join(oracle_mod):
                    got["next_obs"][sel].astype(np.uint32), got["done"][sel]) == \
             key(ref["obs"], ref["action"], ref["reward"], ref["next_obs"], ref["done"])
     env.close()
+
+
+@pytest.mark.parametrize("name,ping,train", [("abilene", 1, 0), ("abilene", 0, 1), ("geant", 1, 0)])
+def test_dqn_buffer_in_kernel_parity(oracle_mod, name, ping, train):
+    """PRISMA_POLICY_DQN_BUFFER: the in-kernel DQN_buffer_model decides exactly like the
+    oracle's fixed-order restatement (and hence like torch up to near-ties)."""
+    from prisma_amd.policies import StackedQNet
+    topo = Topology.example(name)
+    net = StackedQNet(topo, "buffer", seed=21)
+    w = net.pack()
+    params = engine_params(topo, sim_time_s=10.0, ping_as_obs=ping, train=train, replica_base=3)
+    R, H = 4, 2000
+    eng = PrismaEngine(topo, params, R)
+    eng.reset(0)
+    eng.run(w, H // 2)
+    eng.run(w, H // 2)                       # a pending decision carried across launches
+    torch.cuda.synchronize()
+    cnt = eng.counters()
+    log = eng.log_tensor().cpu().numpy()
+    wh = w.cpu().numpy()
+    for r in range(R):
+        o = oracle_mod.OracleSim(topo, params, replica=3 + r)
+        o.run_mlp(wh, H)
+        ref = o.records()
+        assert cnt[r]["error"] == 0
+        assert int(cnt[r]["dec_count"]) == len(ref)
+        assert eng.records(r, 0, len(ref), log_host=log).tobytes() == ref.tobytes(), r
+        assert_counters_equal(cnt[r], o.counters(), r)
+    # the decisions are torch's argmin on the logged observations (up to near-ties)
+    recs = eng.records(0, 0, int(cnt[0]["dec_count"]), log_host=log)
+    dec = recs[(recs["status"] == 1) | (recs["status"] == 2)]
+    obs = torch.from_numpy(dec["obs"].astype(np.int64)).int().cuda()
+    node = torch.from_numpy(dec["node"].astype(np.int64)).cuda()
+    ta = net.act(obs, node).cpu().numpy()
+    assert (ta == dec["action"]).mean() > 0.99
+    eng.close()

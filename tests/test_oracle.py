@@ -261,3 +261,40 @@ def test_train_echo_changes_dynamics_and_counts(oracle_mod):
     extra = int(cb["bytes_signaling"]) - int(ca["bytes_signaling"])
     assert extra > 0 and int(cb["seq"]) > int(ca["seq"])
     assert relayed > 0
+
+
+def test_det_expm1_accuracy(oracle_mod):
+    import math
+    xs = [0.0, -1e-300, -1e-12, -1e-6, -0.01, -0.3, -0.35, -0.5, -1.0, -2.0, -7.3, -20.0, -59.0, -80.0]
+    xs += list(-np.random.default_rng(0).exponential(2.0, 2000))
+    for x in xs:
+        got, want = oracle_mod.det_expm1(x), math.expm1(x)
+        assert abs(got - want) <= 4e-16 * max(1.0, abs(want)) + 1e-300, (x, got, want)
+
+
+def test_oracle_mlp_matches_torch_dqn_buffer(oracle_mod):
+    """The oracle's fixed-order fp32 DQN_buffer_model picks torch's argmin (models.py:258-306)
+    except on near-ties (different summation order)."""
+    import torch
+    from prisma_amd.policies import StackedQNet
+    topo = Topology.example("abilene")
+    net = StackedQNet(topo, "buffer", seed=3, device="cpu")
+    w = net.pack().numpy()
+    p = engine_params(topo, sim_time_s=1.0)
+    s = oracle_mod.OracleSim(topo, p)
+    rng = np.random.default_rng(1)
+    B = 3000
+    node = rng.integers(0, topo.n_nodes, B)
+    obs = np.zeros((B, 1 + topo.max_deg), dtype=np.int64)
+    obs[:, 0] = rng.integers(0, topo.n_nodes, B)
+    obs[:, 1:] = rng.integers(0, 16260, (B, topo.max_deg))
+    ta = net.act(torch.from_numpy(obs).int(), torch.from_numpy(node)).numpy()
+    with torch.no_grad():
+        q = net.q_values(torch.from_numpy(obs).int(), torch.from_numpy(node)).numpy()
+    mism = 0
+    for b in range(B):
+        a = s.mlp_action(w, int(node[b]), obs[b].astype(np.uint32))
+        if a != ta[b]:
+            mism += 1
+            assert abs(q[b, a] - q[b, ta[b]]) <= 1e-5 * max(1.0, abs(q[b, a])), (b, a, ta[b], q[b])
+    assert mism <= B // 100
