@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PRISMA_ABI_VERSION 4
+#define PRISMA_ABI_VERSION 5
 
 /* status codes */
 #define PRISMA_OK              0
@@ -59,12 +59,16 @@ extern "C" {
 #define PRISMA_ERR_STATE      -6   /* call not valid in current state      */
 
 /* policy modes for prisma_run (fused decision) */
-#define PRISMA_POLICY_TABLE    1   /* action = table[node * n_nodes + dst] */
+#define PRISMA_POLICY_TABLE    1   /* action = table[node * n_nodes + dst]
+                                      (underlay ids)                       */
 #define PRISMA_POLICY_DQN_BUFFER 2 /* in-kernel DQN_buffer_model (models.py:258-306)
                                       over packed fp32 weights, D = max_deg:
                                       W1[N][N][32] b1[N][32] Wb[N][D][32] bb[N][32]
                                       W2[N][64][64] b2[N][64] W3[N][64][64] b3[N][64]
-                                      W4[N][64][D] b4[N][D]; x @ W convention     */
+                                      W4[N][64][D] b4[N][D]; x @ W convention;
+                                      N = n_nodes, rows by underlay id; the
+                                      one-hot input is obs[0] (the overlay
+                                      index of the destination)               */
 
 /* per-decision status (prisma_record_t.status) */
 #define PRISMA_ST_PENDING      0   /* waiting for an action (prisma_step)  */
@@ -76,20 +80,33 @@ extern "C" {
 /* runtime error bits (prisma_counters_t.error) */
 #define PRISMA_EBIT_RING       1u  /* link ring overflow                   */
 #define PRISMA_EBIT_WIRE       2u  /* more packets on a wire than sized    */
-#define PRISMA_EBIT_ACKORDER   4u  /* ping-back arrived out of order       */
+#define PRISMA_EBIT_ACKORDER   4u  /* ping-back acknowledging a round more
+                                      than 64 rounds behind a lost one     */
 #define PRISMA_EBIT_TIME       8u  /* time beyond the representable range  */
 #define PRISMA_EBIT_LOGWRAP   16u  /* a hop outlived log_capacity decisions */
+#define PRISMA_EBIT_PINGIDX   32u  /* a ping-back crossing an overlay node
+                                      carried a tunnel index beyond that
+                                      node's degree (out of range of the
+                                      reference's vectors: undefined there) */
 
 /*
- * Topology of one replica (identity overlay: every underlay node is an
- * overlay node, overlay adjacency == physical adjacency).  Directed
- * switch links are numbered in CSR order: links row_ptr[u] ..
- * row_ptr[u+1]-1 leave node u towards link_dst[] in ascending neighbour
- * id, which is the action order of the reference (sim.cc:469-476,
- * forwarder.py:191).  link_rev[l] is the opposite direction of l.
- * Flows are listed in (src, dst) lexicographic order with their
- * load-scaled integer bit rate ceil(trunc_parse(TM[s][d]) * load_factor)
- * (sim.cc:599-631, ns-3 DataRate parse).
+ * Topology of one replica.  Directed switch links (the PHYSICAL underlay)
+ * are numbered in CSR order: links row_ptr[u] .. row_ptr[u+1]-1 leave node
+ * u towards link_dst[] in ascending neighbour id.  link_rev[l] is the
+ * opposite direction of l.  Flows are listed in (src, dst) lexicographic
+ * order of underlay ids, overlay pairs only, with their load-scaled integer
+ * bit rate ceil(trunc_parse(TM[s][d]) * load_factor) (sim.cc:494-514,
+ * 599-631, ns-3 DataRate parse).
+ *
+ * Overlay (sim.cc:455-476): n_overlay = 0 means the identity overlay (every
+ * node is an overlay node, overlay adjacency == physical adjacency, the
+ * abilene / geant examples).  Otherwise overlay_nodes[i] is the underlay id
+ * of overlay node i (the inverse of map_overlay.txt) and overlay_adj the
+ * [n_overlay][n_overlay] 0/1 overlay adjacency.  The actions of overlay node
+ * u are its overlay neighbours in ascending overlay index; an action is a
+ * TUNNEL along the underlay route ns-3 global routing installs (unit
+ * metrics: at every hop the lowest-id neighbour on a shortest path, computed
+ * by the library).  max_deg is the largest overlay degree.
  */
 typedef struct prisma_topology {
     int32_t n_nodes;
@@ -102,6 +119,9 @@ typedef struct prisma_topology {
     const int32_t*  flow_src;   /* [n_flows]                               */
     const int32_t*  flow_dst;   /* [n_flows]                               */
     const uint64_t* flow_rate_bps; /* [n_flows], > 0                       */
+    int32_t n_overlay;          /* 0: identity overlay                     */
+    const int32_t* overlay_nodes;  /* [n_overlay] underlay ids            */
+    const int32_t* overlay_adj;    /* [n_overlay * n_overlay] 0/1         */
 } prisma_topology_t;
 
 /* scenario parameters (argument_parser.py:34-94 defaults in brackets) */
@@ -156,7 +176,10 @@ typedef struct prisma_record {
                                    start-time tag, packet-manager.cc)       */
     int8_t   action;
     uint8_t  status;
-    uint16_t episode;
+    uint8_t  ttl;               /* IP TTL the packet arrived with (255 from
+                                   its app; -1 per intermediate underlay hop
+                                   of a tunnel, Ipv4L3Protocol::IpForward)  */
+    uint8_t  episode;           /* episode index mod 256                   */
     uint32_t obs[];             /* [obs_width]                             */
 } prisma_record_t;
 
@@ -190,6 +213,11 @@ typedef struct prisma_counters {
     uint32_t episode_over;      /* 1 once the current episode ended        */
     uint64_t hops_total;        /* hops over all episodes since reset      */
     uint64_t events_total;      /* events over all episodes since reset    */
+    float    un_cost_sum;       /* running float sum of m_globalUnderlayCost
+                                   (loss penalties of data packets dropped
+                                   at their own destination node, which a
+                                   tunnel can cross)                       */
+    int32_t  un_cost_n;
 } prisma_counters_t;
 
 /* library-owned device buffers (valid until prisma_destroy) */

@@ -34,6 +34,10 @@ class OrConfig(C.Structure):
         ("ma_size", C.c_uint32), ("ping_as_obs", C.c_uint32), ("auto_reset", C.c_uint32),
         ("loss_penalty", C.c_double), ("seed", C.c_uint64), ("replica", C.c_uint32),
         ("episode", C.c_uint32), ("notify_dest", C.c_uint32), ("train", C.c_uint32),
+        ("n_overlay", C.c_int32), ("n_tunnels", C.c_int32),
+        ("overlay_nodes", C.POINTER(C.c_int32)), ("overlay_index", C.POINTER(C.c_int32)),
+        ("ov_row_ptr", C.POINTER(C.c_int32)), ("tun_dst", C.POINTER(C.c_int32)),
+        ("tun_link", C.POINTER(C.c_int32)), ("next_link", C.POINTER(C.c_int32)),
     ]
 
 
@@ -136,6 +140,20 @@ class OracleSim:
         cfg.episode = int(episode)
         cfg.notify_dest = int(params.get("notify_dest", 0))
         cfg.train = int(params.get("train", 0))
+        cfg.n_overlay = topo.n_overlay
+        cfg.n_tunnels = topo.n_tunnels
+        cfg.overlay_nodes = arr(topo.overlay_nodes, C.c_int32, np.int32)
+        cfg.overlay_index = arr(topo.overlay_index, C.c_int32, np.int32)
+        cfg.ov_row_ptr = arr(topo.ov_row_ptr, C.c_int32, np.int32)
+        cfg.tun_dst = arr(topo.tun_dst, C.c_int32, np.int32)
+        cfg.tun_link = arr(topo.tun_link, C.c_int32, np.int32)
+        n = topo.n_nodes
+        nl = np.full((n, n), -1, dtype=np.int32)
+        for x in range(n):
+            for y in range(n):
+                if x != y:
+                    nl[x, y] = topo.link_id(x, int(topo.next_hop[x, y]))
+        cfg.next_link = arr(nl, C.c_int32, np.int32)
         self._cfg = cfg
         self.W = topo.obs_width
         self.rec_dtype = record_dtype(self.W)

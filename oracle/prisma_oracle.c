@@ -2,7 +2,7 @@
  * prisma_oracle.c — TEST INFRASTRUCTURE ONLY (see prisma_oracle.h).
  *
  * Literal single-replica restatement of the reference's ns-3 scenario for
- * identity overlays.  Every handler cites the reference callback it
+ * identity and tunnelled overlays.  Every handler cites the reference callback it
  * restates (paths relative to the reference root, prisma/ns3/ unless
  * noted).  ns-3 upstream semantics that are not in the reference tree are
  * stated from the ns-3 API:
@@ -110,7 +110,7 @@ static double py_reward(int64_t t1, int64_t t0) {
 /* ------------------------------------------------------------------ */
 typedef struct {
     int64_t t_ns; uint32_t uid; int32_t prev; double reward;
-    uint8_t node; uint8_t dst; uint16_t start_s; int8_t action; uint8_t status; uint16_t episode;
+    uint8_t node; uint8_t dst; uint16_t start_s; int8_t action; uint8_t status; uint8_t ttl; uint8_t episode;
 } rec_head_t;
 
 typedef struct {
@@ -123,6 +123,7 @@ typedef struct {
     int32_t cost_n, e2e_n;
     uint32_t episode, ping_rounds, seq, uid, dec_count, ctrl_dropped, error, episode_over;
     uint64_t hops_total, events_total;
+    float un_cost_sum; int32_t un_cost_n;
 } counters_t;
 
 enum { ST_PENDING = 0, ST_ENQUEUED = 1, ST_DROPPED = 2, ST_DEST = 3, ST_DISCARDED = 4 };
@@ -137,7 +138,8 @@ typedef struct {              /* MyTag (my-tag.h:49-65) + size */
     uint64_t start_time;      /* data: whole seconds; ping: ms          */
     int valable;
     uint32_t uid, ping_idx;
-    int tunnel;
+    int tunnel;               /* ping: the origin's local tunnel index      */
+    int ttl;                  /* IP TTL (data: 255 at the app, :330)       */
     float one_hop_delay;
     uint32_t size;            /* bytes incl. PPP header                 */
     int next_free;
@@ -178,7 +180,7 @@ struct or_sim {
     int* flow_draws;
     double* flow_mean;
     uint32_t* ping_index;       /* per node m_pingPacketIndex            */
-    sentvec_t* unacked;         /* per directed link (node, tunnel)      */
+    sentvec_t* unacked;         /* per tunnel (node, local index)        */
     fvec_t* delays;
     uvec_t* lost;               /* per node m_lostPackets (uids)         */
     temp_t* temp; int64_t temp_cap;
@@ -374,8 +376,10 @@ static int dev_send(or_sim_t* s, int di, int p) {                   /* :595-666 
         if (k->valable && k->dst != d->from_node) {
             s->cnt.ov_lost++;
             add_loss_penalty_to_cost(s);
-        } else {
+        } else {                      /* e.g. a tunnel crossing the packet's destination */
             s->cnt.un_lost++;
+            s->cnt.un_cost_sum += (float)s->c.loss_penalty;      /* addLossPenaltyToUnderlayCost */
+            s->cnt.un_cost_n++;
         }
         mac_tx_drop(s, di, p);
     } else {
@@ -409,10 +413,11 @@ static uint32_t ping_obs_value(or_sim_t* s, int l) {
 
 static void observation(or_sim_t* s, int v, int dst, uint32_t* obs) {
     for (int i = 0; i < s->W; ++i) obs[i] = 0;
-    obs[0] = (uint32_t)dst;                          /* identity map_overlay */
-    for (int k = s->c.row_ptr[v]; k < s->c.row_ptr[v + 1]; ++k) {
-        uint32_t val = s->c.ping_as_obs ? ping_obs_value(s, k) : s->dev[k].nbytes;
-        obs[1 + k - s->c.row_ptr[v]] = val;
+    obs[0] = (uint32_t)s->c.overlay_index[dst];      /* m_map_overlay_array[m_destination] */
+    for (int t = s->c.ov_row_ptr[v]; t < s->c.ov_row_ptr[v + 1]; ++t) {
+        /* the device RouteOutput picks for 10.2.2.(nbr+1): the tunnel's first link */
+        uint32_t val = s->c.ping_as_obs ? ping_obs_value(s, t) : s->dev[s->c.tun_link[t]].nbytes;
+        obs[1 + t - s->c.ov_row_ptr[v]] = val;
     }
 }
 
@@ -476,30 +481,35 @@ static void build_ctrl_info(or_sim_t* s, const pkt_t* k, int v) {
 static void send_ping_packets(or_sim_t* s, int u) {                 /* data-packet-manager.cc:350-357 */
     uint32_t idx = s->ping_index[u];
     uint64_t ms = (uint64_t)(s->now / 1000000);                       /* GetMilliSeconds */
-    for (int l = s->c.row_ptr[u]; l < s->c.row_ptr[u + 1]; ++l) {     /* addSentPingForwardPacket */
+    const int t0 = s->c.ov_row_ptr[u], t1 = s->c.ov_row_ptr[u + 1];
+    for (int t = t0; t < t1; ++t) {                                    /* addSentPingForwardPacket */
         sent_t e = { idx, ms };
-        VEC_PUSH(&s->unacked[l], e);
+        VEC_PUSH(&s->unacked[t], e);
     }
-    for (int l = s->c.row_ptr[u]; l < s->c.row_ptr[u + 1]; ++l) {     /* sendPingForwardPacket :360-413 */
+    for (int t = t0; t < t1; ++t) {                                    /* sendPingForwardPacket :360-413 */
         int p = pkt_alloc(s);
         pkt_t* k = &s->pk[p];
         k->type = PING_FORWARD_PACKET;
-        k->dst = k->next_hop = s->c.link_dst[l];
+        k->dst = k->next_hop = s->c.tun_dst[t];
         k->last_hop = k->src = u;
         k->start_time = ms;
-        k->tunnel = l - s->c.row_ptr[u];
+        k->tunnel = t - t0;
         k->ping_idx = idx;
+        k->ttl = 64;                                  /* Ipv4Header default */
         k->size = 8 + 8 + 20 + 2;
-        dev_send(s, l, p);
+        dev_send(s, s->c.tun_link[t], p);             /* RouteOutput(10.2.2.(nbr+1)) */
     }
     s->ping_index[u] = idx + 1;
-    if (u == 0) s->cnt.ping_rounds++;
+    if (u == s->c.overlay_nodes[0]) s->cnt.ping_rounds++;
     schedule(s, s->now + s->ping_period, EV_PING, u, -1);
 }
 
-static void ping_forward_receive(or_sim_t* s, int l_in, int p) {    /* ping-forward-packet-manager.cc:94-156 */
+/* PingForwardPacketManager::receivePacket (ping-forward-packet-manager.cc:94-156) at overlay
+ * node v -- the addressee, or any overlay node the ping crosses (NotifyPktRcv hands every
+ * PING_FORWARD seen on an overlay node's devices to its manager, packet-routing-gym.cc:254-256):
+ * a ping-back to the ping's last hop, on the device it arrived on. */
+static void ping_forward_receive(or_sim_t* s, int v, int l_in, int p) {
     const pkt_t* k = &s->pk[p];
-    int v = s->c.link_dst[l_in];
     float delay = (float)(get_seconds(s->now) - ((double)k->start_time * 0.001));
     int q = pkt_alloc(s);
     pkt_t* b = &s->pk[q];
@@ -510,14 +520,21 @@ static void ping_forward_receive(or_sim_t* s, int l_in, int p) {    /* ping-forw
     b->one_hop_delay = delay;
     b->ping_idx = k->ping_idx;
     b->tunnel = k->tunnel;
+    b->ttl = 64;
     b->size = 8 + 8 + 20 + 2;
     dev_send(s, s->c.link_rev[l_in], q);          /* m_receivingNetDev->Send */
 }
 
-static void ping_back_receive(or_sim_t* s, int l_in, int p) {       /* ping-back-packet-manager.cc:120-144 */
+/* PingBackPacketManager::receivePacket (ping-back-packet-manager.cc:120-144) at overlay node
+ * v, the addressee or a node the ping-back crosses (packet-routing-gym.cc:257-259): the
+ * tunnel index is the ORIGIN's, applied to v's own tunnel list.  An index past v's overlay
+ * degree is out of range of the reference's vectors (undefined behaviour there): flagged
+ * as an error and ignored. */
+static void ping_back_receive(or_sim_t* s, int v, int p) {
     const pkt_t* k = &s->pk[p];
-    int u = s->c.link_dst[l_in];
-    int l = s->c.row_ptr[u] + k->tunnel;
+    const int deg = s->c.ov_row_ptr[v + 1] - s->c.ov_row_ptr[v];
+    if (k->tunnel >= deg) { s->cnt.error |= 32u; s->over = 1; return; }   /* PRISMA_EBIT_PINGIDX */
+    int l = s->c.ov_row_ptr[v] + k->tunnel;
     sentvec_t* uv = &s->unacked[l];
     for (int i = 0; i < uv->n; ++i) {
         if (uv->a[i].idx == k->ping_idx) { vec_erase(uv->a, &uv->n, sizeof(sent_t), i); break; }
@@ -525,6 +542,19 @@ static void ping_back_receive(or_sim_t* s, int l_in, int p) {       /* ping-back
     fvec_t* dv = &s->delays[l];
     if ((uint32_t)dv->n >= s->c.ma_size) vec_erase(dv->a, &dv->n, sizeof(float), 0);
     VEC_PUSH(dv, k->one_hop_delay);
+}
+
+/* Ipv4L3Protocol::IpForward along the global-routing host route to the packet's next hop
+ * (its IP destination 10.2.2.(nextHop+1)) through the patched Ipv4Interface::Send
+ * (ipv4-interface.cc:213-229).  The TTL is decremented first; at 0 the packet is dropped
+ * without any MacTxDrop / counter (the ICMP time-exceeded reply is not modelled). */
+static void ip_forward(or_sim_t* s, int v, int p) {
+    pkt_t* k = &s->pk[p];
+    if (k->type == DATA_PACKET) {
+        k->ttl -= 1;
+        if (k->ttl == 0) { pkt_free(s, p); return; }
+    }
+    dev_send(s, s->c.next_link[(size_t)v * s->N + k->next_hop], p);
 }
 
 /* DataPacketManager::sendSmallSignalingPacket (data-packet-manager.cc:301-347),
@@ -541,6 +571,7 @@ static void send_small_signaling(or_sim_t* s, const pkt_t* data, int v, int l_in
     e->uid = data->uid;                               /* SetIdValue(m_packetUid) */
     e->start_time = 0;
     e->valable = 0;
+    e->ttl = 64;
     e->size = 0 + 8 + 20 + 2;
     dev_send(s, s->c.link_rev[l_in], q);               /* m_receivingNetDev->Send */
 }
@@ -567,6 +598,7 @@ static void flow_send_packet(or_sim_t* s, int f) {                  /* poisson-a
     k->start_time = (uint64_t)get_seconds(s->now);                    /* :310 */
     k->valable = 1;                                                   /* overlay pair: p = 1.0 */
     k->uid = s->next_uid++;
+    k->ttl = 255;                                                     /* SetIpTtl(255) :330 */
     k->size = s->c.packet_size + 8 + 20 + 2;
     dev_send(s, s->E + s->c.flow_src[f], p);                          /* UDP socket -> access link */
     flow_schedule_next(s, f);
@@ -615,24 +647,24 @@ static void finish_data_decision(or_sim_t* s, int action) {
     }
     pkt_t orig = s->pk[p];
     send_small_signaling(s, &orig, v, s->pend_link);
-    int deg = s->c.row_ptr[v + 1] - s->c.row_ptr[v];
+    const int t0 = s->c.ov_row_ptr[v], deg = s->c.ov_row_ptr[v + 1] - t0;
     rec_head_t* r = rec_at(s, d);
     r->action = (int8_t)action;
     if (action >= 0 && action < deg) {
-        int l = s->c.row_ptr[v] + action;
+        const int t = t0 + action;
         int q = pkt_alloc(s);
         pkt_t* k = &s->pk[q];
         *k = s->pk[p];
         k->next_free = -2;
         k->last_hop = v;
-        k->next_hop = s->c.link_dst[l];
+        k->next_hop = s->c.tun_dst[t];
         k->size = s->c.packet_size + 8 + 20 + 2;
         temp_t* tp = temp_of(s, k->uid);
         tp->dec = d; tp->t_ns = s->now; tp->active = 1;
         rec_at(s, d)->status = ST_ENQUEUED;
         s->cnt.hops++;
         s->cnt.hop_deg_sum += (uint64_t)deg;
-        dev_send(s, l, q);              /* a drop re-marks the record DROPPED */
+        dev_send(s, s->c.tun_link[t], q);   /* RouteOutput device; a drop re-marks the record DROPPED */
     } else {
         rec_at(s, d)->status = ST_DISCARDED;
     }
@@ -643,15 +675,20 @@ static void finish_data_decision(or_sim_t* s, int action) {
 
 /* PointToPointNetDevice::Receive -> PacketRoutingEnv::NotifyPktRcv
  * (point-to-point-net-device.cc:371-467, packet-routing-gym.cc:231-267).
- * Returns 1 when a data decision needs an action. */
+ * Order at the receiving switch v: MacRx trace (the overlay node's managers),
+ * then the IP stack (forwarding when v is not the packet's next hop), then
+ * the Receive counters.  Returns 1 when a data decision needs an action. */
 static int receive(or_sim_t* s, int di, int p) {
     const netdev_t* d = &s->dev[di];
     int v = d->to_node;
     pkt_t* k = &s->pk[p];
+    const int overlay = s->c.overlay_index[v] >= 0;
     if (k->type == DATA_PACKET) {
         if (!(k->next_hop == v && k->valable)) {                      /* packet-manager.cc:115 */
-            receive_counters(s, k, v);
-            pkt_free(s, p);
+            pkt_t orig = *k;
+            if (k->next_hop != v) ip_forward(s, v, p);                /* inside a tunnel */
+            else pkt_free(s, p);
+            receive_counters(s, &orig, v);
             return 0;
         }
         int64_t dn = rec_new(s);
@@ -662,7 +699,8 @@ static int receive(or_sim_t* s, int di, int p) {
         r->node = (uint8_t)v;
         r->dst = (uint8_t)k->dst;
         r->start_s = (uint16_t)k->start_time;
-        r->episode = (uint16_t)s->c.episode;
+        r->ttl = (uint8_t)k->ttl;
+        r->episode = (uint8_t)s->c.episode;
         r->action = -1;
         if (tp->active) {                                             /* handle_transit_packet */
             r->prev = (int32_t)tp->dec;
@@ -702,11 +740,15 @@ static int receive(or_sim_t* s, int di, int p) {
                 return 1;
             }
         }
+    } else if (overlay && k->type == PING_FORWARD_PACKET) {
+        ping_forward_receive(s, v, di, p);
+    } else if (overlay && k->type == PING_BACK_PACKET) {
+        ping_back_receive(s, v, p);
     }
-    if (k->type == PING_FORWARD_PACKET) ping_forward_receive(s, di, p);
-    else if (k->type == PING_BACK_PACKET) ping_back_receive(s, di, p);
-    receive_counters(s, &s->pk[p], v);
-    pkt_free(s, p);
+    pkt_t orig = s->pk[p];
+    if (k->next_hop != v) ip_forward(s, v, p);                        /* inside a tunnel */
+    else pkt_free(s, p);
+    receive_counters(s, &orig, v);
     return 0;
 }
 
@@ -766,14 +808,14 @@ or_sim_t* or_create(const or_config_t* cfg) {
     for (int f = 0; f < s->F; ++f)
         s->flow_mean[f] = (double)(cfg->packet_size * 8u) / (double)cfg->flow_rate_bps[f];
     s->ping_index = calloc((size_t)s->N, sizeof(uint32_t));
-    s->unacked = calloc((size_t)s->E + 1, sizeof(sentvec_t));
-    s->delays = calloc((size_t)s->E + 1, sizeof(fvec_t));
+    s->unacked = calloc((size_t)cfg->n_tunnels + 1, sizeof(sentvec_t));
+    s->delays = calloc((size_t)cfg->n_tunnels + 1, sizeof(fvec_t));
     s->lost = calloc((size_t)s->N, sizeof(uvec_t));
     s->cnt.episode = cfg->episode;
     /* setup-time schedule: ping timers (sim.cc:544 -> data-packet-manager.cc:118-121)
        in overlay order, then application starts (Node::Initialize at t=0) in
        flow (src, dst) order (sim.cc:599-631) */
-    for (int u = 0; u < s->N; ++u) schedule(s, s->ping_period, EV_PING, u, -1);
+    for (int i = 0; i < cfg->n_overlay; ++i) schedule(s, s->ping_period, EV_PING, cfg->overlay_nodes[i], -1);
     uint32_t key[2] = { (uint32_t)cfg->seed, cfg->replica };
     for (int f = 0; f < s->F; ++f) {
         uint32_t ctr[4] = { (uint32_t)f, 0u, cfg->episode, 0u };
@@ -789,7 +831,7 @@ or_sim_t* or_create(const or_config_t* cfg) {
 void or_destroy(or_sim_t* s) {
     if (!s) return;
     for (int i = 0; i < s->E + s->N; ++i) free(s->dev[i].q);
-    for (int l = 0; l < s->E; ++l) { free(s->unacked[l].a); free(s->delays[l].a); }
+    for (int t = 0; t < s->c.n_tunnels; ++t) { free(s->unacked[t].a); free(s->delays[t].a); }
     for (int u = 0; u < s->N; ++u) free(s->lost[u].a);
     free(s->dev); free(s->flow_draws); free(s->flow_mean); free(s->ping_index);
     free(s->unacked); free(s->delays); free(s->lost); free(s->temp);
@@ -865,8 +907,8 @@ static int mlp_action(const or_sim_t* s, const float* w, int v, const uint32_t* 
     const float* b3 = W3 + (size_t)N * 64 * 64;
     const float* W4 = b3 + (size_t)N * 64;
     const float* b4 = W4 + (size_t)N * 64 * D;
-    int deg = s->c.row_ptr[v + 1] - s->c.row_ptr[v];
-    int dst = (int)obs[0];
+    int deg = s->c.ov_row_ptr[v + 1] - s->c.ov_row_ptr[v];
+    int dst = (int)obs[0];                                   /* overlay index (one-hot input) */
     float x[128], xn[128], h[64], h2[64];
     float sum = 0.0f, var = 0.0f;
     for (int k = 0; k < deg; ++k) { x[k] = (float)obs[1 + k]; sum = sum + x[k]; }

@@ -1,7 +1,8 @@
 /*
  * prisma_oracle.h — TEST INFRASTRUCTURE ONLY.
  *
- * CPU restatement of the reference's ns-3 packet-hop semantics, used as the
+ * CPU restatement of the reference's ns-3 packet-hop semantics (identity and
+ * tunnelled overlays), used as the
  * parity checker for the HIP engine (tests/, __graft_entry__.smoke() and
  * bench.py's cpu_baseline leg only; never linked into the product).
  *
@@ -48,6 +49,16 @@ typedef struct or_config {
                                    their action is ignored                 */
     uint32_t train;             /* --train: small-signalling echo per data
                                    notification at a non-source node       */
+    /* overlay (sim.cc:455-476): decisions at overlay nodes over tunnels;
+       identity overlays: n_overlay = n_nodes, tunnel t == link t          */
+    int32_t n_overlay, n_tunnels;
+    const int32_t* overlay_nodes;   /* [n_overlay] underlay id, overlay order */
+    const int32_t* overlay_index;   /* [n_nodes] overlay index or -1         */
+    const int32_t* ov_row_ptr;      /* [n_nodes + 1] tunnels of node u       */
+    const int32_t* tun_dst;         /* [n_tunnels] overlay neighbour         */
+    const int32_t* tun_link;        /* [n_tunnels] first physical link       */
+    const int32_t* next_link;       /* [n_nodes * n_nodes] link x -> towards y
+                                       (ns-3 global routing, -1 if x == y)   */
 } or_config_t;
 
 typedef struct or_sim or_sim_t;

@@ -57,10 +57,10 @@ def build_parser() -> argparse.ArgumentParser:
 def parse_arguments(argv=None) -> dict:
     params = vars(build_parser().parse_args(argv))
     topo = Topology.example(params["topology_name"], params["traffic_matrix_index"], params["load_factor"])
-    params["numNodes"] = topo.n_nodes
+    params["numNodes"] = topo.n_overlay
     params["topology"] = topo
     params["loss_penalty"] = _loss_penalty(params["max_out_buffer_size"], params["packet_size"],
-                                           params["link_cap"], topo.n_nodes)
+                                           params["link_cap"], topo.n_overlay)
     return params
 
 
@@ -75,7 +75,7 @@ def engine_params(topo: Topology, *, sim_time_s: float = 60.0, seed: int = 100, 
     node sends a small-signalling echo back to its last hop."""
     if log_capacity < 1024 or log_capacity > (1 << 22) or log_capacity & (log_capacity - 1):
         raise ValueError("log_capacity must be a power of two in [1024, 2^22]")
-    lp = _loss_penalty(max_buffer, packet_size, link_cap, topo.n_nodes) if loss_penalty is None else loss_penalty
+    lp = _loss_penalty(max_buffer, packet_size, link_cap, topo.n_overlay) if loss_penalty is None else loss_penalty
     return dict(
         link_bps=int(link_cap), link_delay_ns=int(round(link_delay_ms * 1e6)),
         max_buffer_bytes=int(max_buffer), packet_size=int(packet_size), sim_time_s=float(sim_time_s),

@@ -14,15 +14,19 @@ constexpr uint32_t K_PING = 0u, K_FLOW = 1u, K_COMPLETE = 2u, K_ARRIVE = 3u;
 // 4-byte packet entry of a link ring; type in bits 0-1:
 //   T_RELAY  data packet forwarded by a decision: bits 2-23 = that decision's
 //            index mod 2^22, bits 24-31 = the packet's source node (its uid,
-//            destination, start second and decision time are read back from
-//            the decision record in the HBM log)
+//            destination, start second, TTL, decision time and -- through the
+//            deciding node and action -- its tunnel are read back from the
+//            decision record in the HBM log)
 //   T_FRESH  data packet of a flow app on its access link: bits 2-10 flow,
 //            bit 11 parity of the start second, bits 12-31 uid mod 2^20
 //   T_PFWD / T_PBACK  ping forward / back (enum-and-constants.h:5-11):
-//            bits 2-8 tunnel, bits 9-30 round; the one-hop delay a ping-back
-//            carries sits in a per-tunnel side table (Layout::s_pbd)
+//            bits 2-9 global tunnel id, bits 10-12 responder position on the
+//            tunnel (ping-backs: 0 = first node after the origin), bits 13-30
+//            round mod 2^18; the one-hop delay a ping-back carries sits in a
+//            side table (Layout::s_pbd) keyed by (tunnel, position, round)
 //   echo     small-signalling packet (--train): T_PBACK with bit 31 set,
-//            bits 9-30 = the signalled data packet's uid mod 2^22
+//            bits 2-9 = its destination node (the data packet's last hop),
+//            bits 10-30 = the signalled data packet's uid mod 2^21
 constexpr uint32_t T_RELAY = 0u, T_FRESH = 1u, T_PFWD = 2u, T_PBACK = 3u;
 constexpr uint32_t kEchoBit = 1u << 31;
 __host__ __device__ inline uint32_t ent_type(uint32_t x) { return x & 3u; }
@@ -39,13 +43,19 @@ __host__ __device__ inline uint32_t f_make(uint32_t flow, uint32_t start_parity,
 __host__ __device__ inline uint32_t f_flow(uint32_t x) { return (x >> 2) & 511u; }
 __host__ __device__ inline uint32_t f_parity(uint32_t x) { return (x >> 11) & 1u; }
 __host__ __device__ inline uint32_t f_uid(uint32_t x) { return x >> 12; }
-__host__ __device__ inline uint32_t p_make(uint32_t type, uint32_t tunnel, uint32_t round) {
-    return type | (tunnel << 2) | (round << 9);
+constexpr uint32_t kRoundBits = 18u, kRoundMask = (1u << kRoundBits) - 1u;
+__host__ __device__ inline uint32_t p_make(uint32_t type, uint32_t tunnel, uint32_t pos, uint32_t round) {
+    return type | (tunnel << 2) | (pos << 10) | ((round & kRoundMask) << 13);
 }
-__host__ __device__ inline uint32_t p_tunnel(uint32_t x) { return (x >> 2) & 127u; }
-__host__ __device__ inline uint32_t p_round(uint32_t x) { return (x >> 9) & ((1u << 22) - 1u); }
-__host__ __device__ inline uint32_t e_make(uint32_t uid) { return T_PBACK | kEchoBit | ((uid & ((1u << 22) - 1u)) << 9); }
-__host__ __device__ inline uint32_t e_uid(uint32_t x) { return (x >> 9) & ((1u << 22) - 1u); }
+__host__ __device__ inline uint32_t p_tunnel(uint32_t x) { return (x >> 2) & 255u; }
+__host__ __device__ inline uint32_t p_pos(uint32_t x) { return (x >> 10) & 7u; }
+__host__ __device__ inline uint32_t p_round(uint32_t x) { return (x >> 13) & kRoundMask; }
+constexpr uint32_t kEchoUidMask = (1u << 21) - 1u;
+__host__ __device__ inline uint32_t e_make(uint32_t uid, uint32_t to) {
+    return T_PBACK | kEchoBit | (to << 2) | ((uid & kEchoUidMask) << 10);
+}
+__host__ __device__ inline uint32_t e_uid(uint32_t x) { return (x >> 10) & kEchoUidMask; }
+__host__ __device__ inline uint32_t e_to(uint32_t x) { return (x >> 2) & 255u; }
 constexpr uint32_t kRelayMask = (1u << 22) - 1u, kUidMask = (1u << 20) - 1u;
 
 // pending-notification flags (Hdr::pend_ent[3])
@@ -72,15 +82,17 @@ struct Hdr {                 // 128 bytes at state offset 0
     uint64_t hops_total;
     uint64_t events_total;
     uint32_t pend_uid;       // uid of the pending data packet (echo payload)
-    uint32_t pad[5];
+    uint32_t pend_last;      // its last hop (echo destination)
+    uint32_t pad[4];
 };
 static_assert(sizeof(Hdr) == 128, "Hdr size");
-// LDS offsets of the header, the counters (144 B) and the pending observation
-constexpr uint32_t kOffHdr = 0u, kOffCnt = 128u, kOffObs = 272u;
+// LDS offsets of the header, the counters (152 B) and the pending observation
+constexpr uint32_t kOffHdr = 0u, kOffCnt = 128u, kOffObs = 288u;
 
 // Read-only topology image (HBM, one per engine), fixed-size arrays so every
 // field sits at a compile-time offset from one base pointer: N <= 255,
-// links incl. access links <= 256, flows <= 512 (checked on the host).
+// links incl. access links <= 256, tunnels <= 256, flows <= 512 (checked on
+// the host).  Tunnelled overlays append the routing table route[N][N].
 struct TopoImage {
     int32_t rowptr[256];         // CSR of directed switch links by source node
     int32_t ldst[256];           // far end of link l (access link E+u: u)
@@ -89,7 +101,16 @@ struct TopoImage {
     int32_t fsrc[512];
     int32_t fdst[512];
     double  fmean[512];          // mean inter-arrival of flow f (s)
+    int32_t ovrow[256];          // CSR of tunnels (actions) by node; identity: == rowptr
+    uint32_t tinfo[256];         // tunnel t: first link | target << 8 | origin << 16 | links << 24
+    int32_t ovi[256];            // overlay index of node x (obs[0] of a packet for x), -1 if none
+    int32_t ovnode[256];         // underlay id of overlay node i (ping timers, overlay order)
+    // uint32_t route[N][N] follows (tunnelled overlays only): next link x -> y | hops(x, y) << 8
 };
+__host__ __device__ inline uint32_t ti_link(uint32_t ti) { return ti & 255u; }
+__host__ __device__ inline uint32_t ti_tgt(uint32_t ti) { return (ti >> 8) & 255u; }
+__host__ __device__ inline uint32_t ti_org(uint32_t ti) { return (ti >> 16) & 255u; }
+__host__ __device__ inline uint32_t ti_len(uint32_t ti) { return ti >> 24; }
 
 // Offsets (bytes) of every region; filled on the host, read by the kernels
 // from a device copy.
@@ -98,9 +119,12 @@ struct Layout {
     uint32_t topo_bytes, state_bytes, lds_bytes, table_bytes;
     // state image (LDS offset 0) and the action table (LDS offset lds_state_bytes)
     uint32_t s_hdr, s_cnt, s_obs, s_wt, s_wseq, s_ring, s_win, s_pbd, s_mlp;
+    int32_t  T, NO;              // tunnels, overlay nodes
+    uint32_t tunnels;            // 1: tunnelled overlay (route table present)
+    uint32_t PLEN;               // responder positions per tunnel (max tunnel length)
     uint32_t lds_state_bytes;    // LDS part of the image (bytes [0, lds_state_bytes))
-    uint32_t s_regs;             // register part: 4 x [64*FS] + 20 x [64*LS] u32 arrays
-    uint32_t PBK;                // ping-back delay slots per tunnel (power of two)
+    uint32_t s_regs;             // register part: 4 x [64*FS] + 19 x [64*LS] u32 arrays
+    uint32_t PBK;                // ping-back delay slots per (tunnel, position) (power of two)
     int32_t  FS, LS;             // flow / link register slots per lane
     // link constants (identical on every switch link: sim.cc:414-433)
     int64_t  sw_txd, sw_txp, sw_txe, sw_prop;   // tx of data / ping / echo, propagation

@@ -145,10 +145,12 @@ struct Regs {
     LA<LS> cp_t, cp_seq;                         // tx completion event (valid while busy)
     LA<LS> wh_t, wh_seq;                         // arrival event of the wire head (valid while n_wire > 0)
     LA<LS> p0, p1, p2, qb;                       // head|txp<<16, tail|n_wire<<16, n_queue|busy<<16, queued bytes
-    LA<LS> pm_ack, pm_hole, pm_win;              // ping: last ack, first hole, win_n|win_head<<16
+    // per TUNNEL t (lane t % 64, slot t / 64; tunnel == link on identity overlays):
+    LA<LS> pm_lo, pm_mlo, pm_mhi;                // ping: oldest unacked round, acked bits of rounds lo+1..lo+64
+    LA<LS> pm_win;                               // win_n | win_head << 16 | saturated << 31
     LA<LS> pav_lo, pav_hi;                       // ping window mean (double), refreshed per ping-back
-    LA<LS> nd_lo, nd_hi, hd_lo, hd_hi;           // send time (s) of ping ack+1 and of the first hole
-    static constexpr int NF = 4, NL = 20;
+    LA<LS> od_lo, od_hi;                         // send time (s) of round lo
+    static constexpr int NF = 4, NL = 19;
 };
 
 template <int FS, int LS>
@@ -159,9 +161,9 @@ __device__ __forceinline__ void regs_io(Regs<FS, LS>& R, uint32_t* img, int lane
 #define RIO_L(fld, a) if (store) R.fld.store(lb + (a) * 64 * LS, lane); else R.fld.load(lb + (a) * 64 * LS, lane);
     RIO_F(fk_lo, 0) RIO_F(fk_hi, 1) RIO_F(fk_seq, 2) RIO_F(f_draw, 3)
     RIO_L(lk_t, 0) RIO_L(wh_t, 1) RIO_L(lk_seq, 2) RIO_L(lk_kind, 3) RIO_L(cp_t, 4) RIO_L(wh_seq, 5)
-    RIO_L(cp_seq, 6) RIO_L(p0, 7) RIO_L(p1, 8) RIO_L(p2, 9) RIO_L(qb, 10) RIO_L(pm_ack, 11)
-    RIO_L(pm_hole, 12) RIO_L(pm_win, 13) RIO_L(pav_lo, 14) RIO_L(pav_hi, 15) RIO_L(nd_lo, 16)
-    RIO_L(nd_hi, 17) RIO_L(hd_lo, 18) RIO_L(hd_hi, 19)
+    RIO_L(cp_seq, 6) RIO_L(p0, 7) RIO_L(p1, 8) RIO_L(p2, 9) RIO_L(qb, 10) RIO_L(pm_lo, 11)
+    RIO_L(pm_mlo, 12) RIO_L(pm_mhi, 13) RIO_L(pm_win, 14) RIO_L(pav_lo, 15) RIO_L(pav_hi, 16)
+    RIO_L(od_lo, 17) RIO_L(od_hi, 18)
 #undef RIO_F
 #undef RIO_L
 }
@@ -180,6 +182,7 @@ struct Hot {
 // is wave-uniform, so these become s_load through the scalar cache.
 #define CAS __attribute__((address_space(4)))
 typedef const CAS int32_t c_i32;
+typedef const CAS uint32_t c_u32;
 typedef const CAS int64_t c_i64;
 typedef const CAS double c_f64;
 typedef const CAS Layout CLayout;        // scenario constants: s_load, never clobbered
@@ -217,6 +220,10 @@ struct LV {
     __device__ __forceinline__ uint32_t s_win() const { return (uint32_t)u(offsetof(Layout, s_win) / 4); }
     __device__ __forceinline__ uint32_t s_pbd() const { return (uint32_t)u(offsetof(Layout, s_pbd) / 4); }
     __device__ __forceinline__ uint32_t s_mlp() const { return (uint32_t)u(offsetof(Layout, s_mlp) / 4); }
+    __device__ __forceinline__ int32_t T() const { return (int32_t)u(offsetof(Layout, T) / 4); }
+    __device__ __forceinline__ int32_t NO() const { return (int32_t)u(offsetof(Layout, NO) / 4); }
+    __device__ __forceinline__ uint32_t tunnels() const { return (uint32_t)u(offsetof(Layout, tunnels) / 4); }
+    __device__ __forceinline__ uint32_t PLEN() const { return (uint32_t)u(offsetof(Layout, PLEN) / 4); }
     __device__ __forceinline__ uint32_t lds_state_bytes() const { return (uint32_t)u(offsetof(Layout, lds_state_bytes) / 4); }
     __device__ __forceinline__ uint32_t s_regs() const { return (uint32_t)u(offsetof(Layout, s_regs) / 4); }
     __device__ __forceinline__ uint32_t PBK() const { return (uint32_t)u(offsetof(Layout, PBK) / 4); }
@@ -259,7 +266,7 @@ struct Sim {
     uint32_t* wt; uint32_t* wseq;           // wire: arrival time (low 32 bits) and seq
     uint32_t* ring;
     float* win;
-    float* pbd;                             // ping-back delays [E][PBK]
+    float* pbd;                             // ping-back delays [T][PLEN][PBK]
     const CAS TopoImage* T;                 // topology (scalar loads at fixed offsets)
     const uint8_t* table;
     const float* mlp;                       // DQN-buffer weights (HBM) or null
@@ -472,15 +479,13 @@ __device__ __forceinline__ double ld_d(uint32_t lo, uint32_t hi) {
 }
 
 // 1000 * max(mean(window), min(now - oldest unacknowledged send, 2.6)) of a
-// tunnel (data-packet-manager.cc:171-206).  Acknowledgements of one tunnel
-// arrive in index order, so the oldest pending entry is the first hole below
-// the last ack, else the ping after the last ack if it was sent.  The window
-// mean and both candidate send times are cached per link and refreshed on
-// every ping-back.  Evaluated per lane for the links the lane owns.
-__device__ __forceinline__ uint32_t ping_value_lane(double avg, int32_t hole, int32_t acked, double hd, double nd,
-                                                    uint32_t rounds, double now_s) {
-    const bool pend = hole >= 0 || (int64_t)acked + 1 < (int64_t)rounds;
-    const double od = hole >= 0 ? hd : nd;
+// tunnel (data-packet-manager.cc:171-206).  The unacknowledged list is kept
+// as its oldest round lo (pending iff lo < rounds sent) plus the acked bits
+// of the 64 rounds after it; the window mean and lo's send time are cached
+// per tunnel and refreshed on every ping-back.  Evaluated per lane for the
+// tunnels the lane owns.
+__device__ __forceinline__ uint32_t ping_value_lane(double avg, uint32_t lo, double od, uint32_t rounds, double now_s) {
+    const bool pend = lo < rounds;
     const double a = now_s - od;
     const double b = 2.60;
     const float mt = pend ? (float)((b < a) ? b : a) : 0.0f;
@@ -489,24 +494,31 @@ __device__ __forceinline__ uint32_t ping_value_lane(double avg, int32_t hole, in
 }
 
 // Observation of node v as a per-lane register (lane i holds obs[i], lane 0
-// left 0 for the destination): every lane evaluates the links it owns in
-// parallel, then lane i pulls link rowptr[v] + i - 1 with one permute per
-// register slot.
+// left 0 for the destination): every lane evaluates the tunnels (ping
+// statistic) or links (queued bytes) it owns in parallel, then lane i pulls
+// the value of action i-1 with one permute per register slot.  Action a of v
+// is tunnel ovrow[v] + a; its queue is that of the tunnel's first link
+// (the device RouteOutput picks, data-packet-manager.cc:180-195), which is
+// the tunnel itself on identity overlays.
 template <int FS, int LS>
 __device__ __forceinline__ uint32_t observe_links(const Sim& S, const Regs<FS, LS>& R, const Hot& H, uint32_t v,
                                                   double now_s) {
     if (PRISMA_ABLATE & 4) return 0u;
-    const int r0 = S.T->rowptr[v], deg = S.T->rowptr[v + 1] - r0;
+    const int r0 = S.T->ovrow[v], deg = S.T->ovrow[v + 1] - r0;
     const int lane = S.lane;
-    const uint32_t src = (uint32_t)(r0 + lane - 1);
+    uint32_t src = (uint32_t)(r0 + lane - 1);
+    const bool pobs = S.lv.ping_as_obs() != 0u;
+    if (!pobs && S.lv.tunnels()) {
+        const bool act = lane >= 1 && lane <= deg;
+        src = act ? ti_link(S.T->tinfo[act ? src : 0u]) : 0u;
+    }
     uint32_t o = 0;
 #pragma unroll
     for (int j = 0; j < LS; ++j) {
         uint32_t val;
-        if (S.lv.ping_as_obs())
-            val = ping_value_lane(ld_d(R.pav_lo.v[j], R.pav_hi.v[j]), (int32_t)R.pm_hole.v[j], (int32_t)R.pm_ack.v[j],
-                                  ld_d(R.hd_lo.v[j], R.hd_hi.v[j]), ld_d(R.nd_lo.v[j], R.nd_hi.v[j]), H.ping_rounds,
-                                  now_s);
+        if (pobs)
+            val = ping_value_lane(ld_d(R.pav_lo.v[j], R.pav_hi.v[j]), R.pm_lo.v[j], ld_d(R.od_lo.v[j], R.od_hi.v[j]),
+                                  H.ping_rounds, now_s);
         else
             val = R.qb.v[j];
         const uint32_t g = (uint32_t)__shfl((int)val, (int)(src & 63u));
@@ -518,11 +530,11 @@ __device__ __forceinline__ uint32_t observe_links(const Sim& S, const Regs<FS, L
 // one coalesced wave store of a decision record (lane i writes word i)
 __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_t d, double reward, uint32_t uid,
                                              int32_t prev, uint32_t node, uint32_t dst, uint32_t start, int action,
-                                             uint32_t status, uint32_t obs_reg) {
+                                             uint32_t status, uint32_t obs_reg, uint32_t ttl) {
     if (PRISMA_ABLATE & 2) return;
     const int lane = S.lane;
     uint64_t rb = __double_as_longlong(reward);
-    uint32_t w7 = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
+    uint32_t w7 = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | (ttl << 16) | ((H.episode & 0xffu) << 24);
     uint32_t hw;
     switch (lane) {
     case 0: hw = lo32(H.now); break;
@@ -540,12 +552,17 @@ __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_
     if (lane < 8 + S.lv.W()) p[lane] = word;
 }
 
+// action + status of a record written earlier (TTL and episode bytes kept)
 __device__ __forceinline__ void patch_record(const Sim& S, const Hot& H, uint32_t d, int action, uint32_t status) {
     if (PRISMA_ABLATE & 2) return;
     if (S.lane == 0) {
         unsigned char* p = S.logrep + (size_t)(d & (S.lv.log_cap() - 1)) * S.lv.rec_bytes();
-        *(uint32_t*)(p + 28) = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | ((H.episode & 0xffffu) << 16);
+        *(uint16_t*)(p + 28) = (uint16_t)((uint32_t)(uint8_t)(int8_t)action | (status << 8));
     }
+}
+__device__ __forceinline__ void patch_status(const Sim& S, uint32_t d, uint32_t status) {
+    if (PRISMA_ABLATE & 2) return;
+    if (S.lane == 0) S.logrep[(size_t)(d & (S.lv.log_cap() - 1)) * S.lv.rec_bytes() + 29] = (unsigned char)status;
 }
 
 // Receive tail after the MacRx trace (point-to-point-net-device.cc:430-463).
@@ -579,10 +596,22 @@ __device__ __forceinline__ uint32_t ent_src(const Sim& S, uint32_t x) {
 }
 
 // DataPacketManager::sendSmallSignalingPacket (data-packet-manager.cc:301-347): a 0-B
-// payload (30 B on the wire, signalling type "ideal") back on the arrival device
+// payload (30 B on the wire, signalling type "ideal") back on the arrival device,
+// addressed to the data packet's last hop `to`
 template <int FS, int LS>
-__device__ __forceinline__ void send_echo(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t link, uint32_t uid) {
-    if (!link_send(S, R, H, link, e_make(uid))) CNT_ADD(S, ctrl_dropped, 1u);
+__device__ __forceinline__ void send_echo(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t link, uint32_t uid,
+                                          uint32_t to) {
+    if (!link_send(S, R, H, link, e_make(uid, to))) CNT_ADD(S, ctrl_dropped, 1u);
+}
+
+// routing table of a tunnelled overlay: next link x -> y | hops(x, y) << 8
+__device__ __forceinline__ uint32_t route(const Sim& S, uint32_t x, uint32_t y) {
+    const c_u32* rt = (const c_u32*)((const CAS unsigned char*)S.T + sizeof(TopoImage));
+    return rt[x * (uint32_t)S.lv.N() + y];
+}
+// first link of tunnel t
+__device__ __forceinline__ uint32_t tunnel_link(const Sim& S, uint32_t t) {
+    return S.lv.tunnels() ? ti_link(S.T->tinfo[t]) : t;
 }
 
 // DataPacketManager::sendPacket (data-packet-manager.cc:251-299) for decision
@@ -593,17 +622,17 @@ template <int FS, int LS>
 __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t x, uint32_t dst,
                                                uint32_t start, uint32_t uid, uint32_t v, uint32_t d, int action,
                                                bool fused, double reward, int32_t prev, uint32_t obs_reg,
-                                               uint32_t echo_link) {
+                                               uint32_t echo_link, uint32_t last, uint32_t ttl) {
     const LV& L = S.lv;
 #if PRISMA_TIMING
     S.tlast = TM_NOW();
 #endif
     // ExecuteActions (packet-routing-gym.cc:203-208): the --train echo goes first
-    if (echo_link != kNoLink) send_echo(S, R, H, echo_link, uid);
-    int r0 = S.T->rowptr[v], deg = S.T->rowptr[v + 1] - r0;
+    if (echo_link != kNoLink) send_echo(S, R, H, echo_link, uid, last);
+    int r0 = S.T->ovrow[v], deg = S.T->ovrow[v + 1] - r0;
     uint32_t status;
     if (action >= 0 && action < deg) {
-        uint32_t l = (uint32_t)(r0 + action);
+        const uint32_t l = tunnel_link(S, (uint32_t)(r0 + action));   // RouteOutput (:281-287)
         CNT_ADD(S, hops, 1u);
         CNT_ADD(S, hop_deg_sum, (uint64_t)deg);
         const uint32_t src = ent_src(S, x);
@@ -623,7 +652,7 @@ __device__ __forceinline__ void apply_decision(const Sim& S, Regs<FS, LS>& R, Ho
 #if PRISMA_TIMING
     { const uint64_t t = TM_NOW(); S.tsub[0] += t - S.tlast; S.tlast = t; }
 #endif
-    if (fused) write_record(S, H, d, reward, uid, prev, v, dst, start, action, status, obs_reg);
+    if (fused) write_record(S, H, d, reward, uid, prev, v, dst, start, action, status, obs_reg, ttl);
     else patch_record(S, H, d, action, status);
     receive_counters(S, R, H, x, false, 0u);
 #if PRISMA_TIMING
@@ -645,13 +674,14 @@ __device__ __forceinline__ int finish_pending(const Sim& S, Regs<FS, LS>& R, Hot
         return 0;
     }
     const uint32_t echo_link = (flags & PEND_ECHO) ? (uint32_t)S.T->lrev[u_ld32(&h.pend_link)] : kNoLink;
+    const uint32_t last = u_ld32(&h.pend_last);
     if (flags & PEND_DEST) {
-        if (echo_link != kNoLink) send_echo(S, R, H, echo_link, u_ld32(&h.pend_uid));
+        if (echo_link != kNoLink) send_echo(S, R, H, echo_link, u_ld32(&h.pend_uid), last);
         receive_counters(S, R, H, x, true, u_ld32(&h.pend_ent[2]));
         return 0;
     }
     apply_decision(S, R, H, x, 0u, 0u, u_ld32(&h.pend_uid), u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action,
-                   false, 0.0, 0, 0u, echo_link);
+                   false, 0.0, 0, 0u, echo_link, last, 0u);
     return 1;
 }
 
@@ -661,18 +691,20 @@ __device__ __forceinline__ void on_ping_round(const Sim& S, Regs<FS, LS>& R, Hot
     const LV& L = S.lv;
     uint32_t k = H.ping_rounds;
     uint32_t first_rearm = 0;
-    for (int u = 0; u < L.N(); ++u) {
-        int r0 = S.T->rowptr[u], r1 = S.T->rowptr[u + 1];
-        for (int l = r0; l < r1; ++l) {
-            if (!link_send(S, R, H, (uint32_t)l, p_make(T_PFWD, (uint32_t)(l - r0), k))) CNT_ADD(S, ctrl_dropped, 1u);
+    for (int i = 0; i < L.NO(); ++i) {                            // timers in overlay order (sim.cc:528-546)
+        const int u = S.T->ovnode[i];
+        const int r0 = S.T->ovrow[u], r1 = S.T->ovrow[u + 1];
+        for (int t = r0; t < r1; ++t) {
+            if (!link_send(S, R, H, tunnel_link(S, (uint32_t)t), p_make(T_PFWD, (uint32_t)t, 0u, k)))
+                CNT_ADD(S, ctrl_dropped, 1u);
         }
         uint32_t s = H.seq++;                                    // re-arm of node u
-        if (u == 0) first_rearm = s;
+        if (i == 0) first_rearm = s;
     }
     H.ping_rounds = k + 1;
-    // one ns-3 event per node timer (the round is N consecutive events)
-    CNT_ADD(S, events, (uint64_t)(L.N() - 1));
-    H.ev_launch += (uint32_t)(L.N() - 1);
+    // one ns-3 event per overlay node timer (the round is NO consecutive events)
+    CNT_ADD(S, events, (uint64_t)(L.NO() - 1));
+    H.ev_launch += (uint32_t)(L.NO() - 1);
     H.ping_t = H.now + L.ping_period();
     H.ping_seq = first_rearm;
 }
@@ -716,7 +748,8 @@ __device__ __forceinline__ float mlp_dense64(const Sim& S, const float* __restri
     return acc;
 }
 
-__device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t dst, uint32_t obs_reg) {
+// one-hot input: obs[0] (the destination's overlay index, lane 0 of obs_reg)
+__device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs_reg) {
     const LV& L = S.lv;
     const int lane = S.lane;
     const int N = L.N(), D = L.max_deg();
@@ -730,7 +763,8 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t dst
     const float* __restrict__ b3 = W3 + N * 64 * 64;
     const float* __restrict__ W4 = b3 + N * 64;
     const float* __restrict__ b4 = W4 + N * 64 * D;
-    const int deg = S.T->rowptr[v + 1] - S.T->rowptr[v];
+    const int deg = S.T->ovrow[v + 1] - S.T->ovrow[v];
+    const uint32_t dst = rdl(obs_reg, 0);
     // LayerNormalization of the deg buffer values (population variance, epsilon 1e-3)
     float sum = 0.0f;
     for (int k = 0; k < deg; ++k) sum = __fadd_rn(sum, (float)rdl(obs_reg, (uint32_t)(k + 1)));
@@ -794,8 +828,77 @@ __device__ __forceinline__ void wire_pop(const Sim& S, Regs<FS, LS>& R, const Ho
 }
 
 struct Decision {
-    uint32_t x, dst, start, uid, v, d; double reward; int32_t prev; uint32_t obs, flags;
+    uint32_t x, dst, start, uid, v, d; double reward; int32_t prev; uint32_t obs, flags, last, ttl;
 };
+
+// a control packet (or a data packet inside a tunnel) continues along the
+// underlay route to `to` (Ipv4L3Protocol::IpForward through the patched
+// Ipv4Interface::Send, ipv4-interface.cc:213-229)
+template <int FS, int LS>
+__device__ __forceinline__ void ctrl_forward(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t v, uint32_t to,
+                                             uint32_t x) {
+    if (!link_send(S, R, H, ti_link(route(S, v, to)), x)) CNT_ADD(S, ctrl_dropped, 1u);
+}
+
+// PingBackPacketManager::receivePacket (ping-back-packet-manager.cc:120-144) on
+// tunnel lt with the one-hop delay the ping-back carries
+template <int FS, int LS>
+__device__ __forceinline__ void ping_ack(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t lt, uint32_t rnd,
+                                         float delay) {
+    const LV& L = S.lv;
+    // the round itself (rounds in flight are less than 2^18 behind the last one sent)
+    const uint32_t last = H.ping_rounds - 1u;
+    const uint32_t k = last - ((last - rnd) & kRoundMask);
+    // erase round k from the unacknowledged list (first match; none if already acked)
+    uint32_t lo = R.pm_lo.get(lt);
+    uint64_t mask = ((uint64_t)R.pm_mhi.get(lt) << 32) | R.pm_mlo.get(lt);
+    uint32_t pw = R.pm_win.get(lt);
+    if (k == lo) {
+        if (pw >> 31) fail(H, PRISMA_EBIT_ACKORDER);               // acked bits were lost (see below)
+        const uint32_t n = (uint32_t)__builtin_ctzll(~mask);       // rounds lo+1.. already acked
+        lo += 1u + n;
+        mask = (n >= 63u) ? 0ull : (mask >> (n + 1u));
+        const uint64_t od = __double_as_longlong(ping_send_s(L, lo));
+        R.pm_lo.set(lt, lo);
+        R.od_lo.set(lt, (uint32_t)od);
+        R.od_hi.set(lt, (uint32_t)(od >> 32));
+        R.pm_mlo.set(lt, (uint32_t)mask);
+        R.pm_mhi.set(lt, (uint32_t)(mask >> 32));
+    } else if (k > lo) {
+        const uint32_t b = k - lo - 1u;
+        if (b < 64u) {
+            mask |= 1ull << b;
+            R.pm_mlo.set(lt, (uint32_t)mask);
+            R.pm_mhi.set(lt, (uint32_t)(mask >> 32));
+        } else {
+            pw |= 1u << 31;      // round lo is lost for good unless acked > 64 rounds late
+        }
+    }
+    // tunnelsDelay window (MA newest delays, oldest first)
+    const uint32_t MA = L.ma();
+    uint32_t wn = pw & 0xffffu, wh = (pw >> 16) & 0x7fffu, slot;
+    if (wn >= MA) {
+        slot = wh;
+        wh = (wh + 1 == MA) ? 0 : wh + 1;
+    } else {
+        slot = wh + wn;
+        if (slot >= MA) slot -= MA;
+        wn++;
+    }
+    R.pm_win.set(lt, wn | (wh << 16) | (pw & (1u << 31)));
+    if (S.lane == 0) S.win[lt * MA + slot] = delay;
+    // refresh the cached window mean (data-packet-manager.cc:55-65), summed oldest first
+    double sum = 0.0;
+    uint32_t i = wh;
+    for (uint32_t j = 0; j < wn; ++j) {
+        float w = (i == slot) ? delay : __uint_as_float(u_ld32((const uint32_t*)S.win + lt * MA + i));
+        sum += (double)w;
+        i = (i + 1 == MA) ? 0 : i + 1;
+    }
+    uint64_t avg = __double_as_longlong(sum / (double)wn);
+    R.pav_lo.set(lt, (uint32_t)avg);
+    R.pav_hi.set(lt, (uint32_t)(avg >> 32));
+}
 
 // returns 1 if a data decision needs an action
 template <int FS, int LS>
@@ -805,29 +908,63 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     const uint32_t x = u_ld32(&S.ring[ring_off(L, l) + k.head]);
     const uint32_t type = ent_type(x);
     const uint32_t v = (uint32_t)S.T->ldst[l];
+    const bool tun = L.tunnels() != 0u;
     if (ent_is_data(x)) {
         // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
         // A forwarded packet's previous decision record (t_ns, uid, dst,
-        // start) comes from the HBM log -- the temp_obs entry of
-        // forwarder.py:153-159.  The load is issued first and consumed after
-        // the link update and the observation, which do not depend on it
-        // (and only on this path, so no load is ever left in flight across
-        // loop iterations).
+        // start, deciding node + action, TTL) comes from the HBM log -- the
+        // temp_obs entry of forwarder.py:153-159.  The load is issued first
+        // and consumed after the link update and the observation, which do
+        // not depend on it (and only on this path, so no load is ever left
+        // in flight across loop iterations).
         // (A fresh packet loads and ignores some record of its own log: the
         // load and its consumption are unconditional on this path.)
         const uint32_t d = H.dec;
         const uint32_t dist = (d - r_dec(x)) & kRelayMask;
         const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap() - 1)) * L.rec_bytes();
         const uint4 ph = *(const uint4*)pr;
-        const uint32_t w6 = *(const uint32_t*)(pr + 24);
+        const uint2 pw = *(const uint2*)(pr + 24);
         wire_pop(S, R, H, l, k);
+        uint32_t ttl = 255u;                                        // SetIpTtl(255) (poisson-application.cc:330)
+        if (tun && type == T_RELAY) {
+            // Tunnelled overlay: the packet's next hop is the target of the tunnel
+            // the previous decision picked; anywhere else it is only IP-forwarded
+            // (packet-manager.cc:115 -> not valid, no Notify).
+            const uint32_t w6p = rfl(pw.x), w7p = rfl(pw.y);
+            const uint32_t u = w6p & 255u;
+            const uint32_t ti = S.T->tinfo[(uint32_t)S.T->ovrow[u] + (w7p & 255u)];
+            const uint32_t ttl_prev = (w7p >> 16) & 255u;
+            if (ti_tgt(ti) != v) {
+                if (dist >= L.log_cap()) fail(H, PRISMA_EBIT_LOGWRAP);
+                // IpForward decrements the TTL first and drops at 0 (no trace, no counter)
+                if (ttl_prev == (route(S, u, v) >> 8)) return 0;
+                if (!link_send(S, R, H, ti_link(route(S, v, ti_tgt(ti))), x)) {
+                    // dropped on an intermediate FIFO: point-to-point-net-device.cc:655-664 at this
+                    // node, MacTxDrop -> the sender's loss (data-packet-manager.cc:88-98,
+                    // forwarder.py:214-244)
+                    if (((w6p >> 8) & 255u) != v) {
+                        CNT_ADD(S, ov_lost, 1u);
+                        CNT_ADD(S, cost_sum, L.loss_penalty_f());
+                        CNT_ADD(S, cost_n, 1u);
+                    } else {
+                        CNT_ADD(S, un_lost, 1u);
+                        CNT_ADD(S, un_cost_sum, L.loss_penalty_f());
+                        CNT_ADD(S, un_cost_n, 1u);
+                    }
+                    patch_status(S, d - dist, PRISMA_ST_DROPPED);
+                    CNT_ADD(S, reward_sum, L.loss_penalty());
+                }
+                return 0;
+            }
+            ttl = ttl_prev - (ti_len(ti) - 1u);
+        }
         H.dec = d + 1u;
         const uint32_t obs_links = observe_links(S, R, H, v, ns_to_sec(H.now));
         const int64_t t_prev = mk64(rfl(ph.x), rfl(ph.y));
-        const uint32_t uid_prev = rfl(ph.z), w_prev = rfl(w6);
+        const uint32_t uid_prev = rfl(ph.z), w_prev = rfl(pw.x);
         double reward = 0.0;
         int32_t prev = -1;
-        uint32_t dst, start, uid;
+        uint32_t dst, start, uid, last = 0u;
         if (type == T_FRESH) {
             // first notification: destination from the flow, uid and start
             // second rebuilt from their low bits (the packet left its app less
@@ -836,8 +973,8 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             dst = (uint32_t)S.T->fdst[f];
             const uint32_t s0 = (uint32_t)(H.now / 1000000000);
             start = s0 - ((s0 ^ f_parity(x)) & 1u);
-            const uint32_t last = H.uid - 1u;
-            uid = last - ((last - f_uid(x)) & kUidMask);
+            const uint32_t lu = H.uid - 1u;
+            uid = lu - ((lu - f_uid(x)) & kUidMask);
         } else if (PRISMA_ABLATE & 1) {
             dst = (x >> 2) & 255u; start = x >> 10; uid = 0; prev = (int32_t)d - 1;
         } else {
@@ -846,89 +983,73 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             uid = uid_prev;
             dst = (w_prev >> 8) & 255u;
             start = w_prev >> 16;
+            last = w_prev & 255u;
             reward = (double)py_micros(H.now) / 1e6 - (double)py_micros(t_prev) / 1e6;   // forwarder.py:360
             CNT_ADD(S, reward_sum, reward);
         }
-        const uint32_t o = (S.lane == 0) ? dst : obs_links;
+        const uint32_t o = (S.lane == 0) ? (uint32_t)S.T->ovi[dst] : obs_links;   // m_map_overlay_array[dst]
         CNT_ADD(S, decisions, 1u);
         // --train: the answer to this notification also echoes a small-signalling
         // packet to the last hop, unless this node is the packet's source (:303-306)
         const uint32_t echo = (L.train() && v != ent_src(S, x)) ? PEND_ECHO : 0u;
         D.x = x; D.dst = dst; D.start = start; D.uid = uid; D.v = v; D.d = d; D.reward = reward; D.prev = prev;
-        D.obs = o; D.flags = echo;
+        D.obs = o; D.flags = echo; D.last = last; D.ttl = ttl;
         if (dst == v) {                                             // getGameOver
-            write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_DESTINATION, o);
+            write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_DESTINATION, o, ttl);
             if (!fused && L.notify_dest()) {                        // the agent is notified (done=True)
                 D.flags |= PEND_DEST;
                 return 1;
             }
-            if (echo) send_echo(S, R, H, (uint32_t)S.T->lrev[l], uid);
+            if (echo) send_echo(S, R, H, (uint32_t)S.T->lrev[l], uid, last);
             receive_counters(S, R, H, x, true, start);
             return 0;
         }
-        if (!fused) write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_PENDING, o);
+        if (!fused) write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_PENDING, o, ttl);
         return 1;
     }
     wire_pop(S, R, H, l, k);
     if (ent_is_echo(x)) {
+        const uint32_t to = e_to(x);
+        if (tun && to != v) { ctrl_forward(S, R, H, v, to, x); return 0; }
         // SmallSignalingPacketManager::receivePacket (small-signaling-packet-manager.cc:86-94):
         // addressed to this node, so valid -> Notify; the agent sees obs [1000]
         if (!fused && L.notify_dest()) {
-            D.x = x; D.v = v; D.uid = e_uid(x); D.flags = PEND_CTRL;
+            D.x = x; D.v = v; D.uid = e_uid(x); D.flags = PEND_CTRL; D.last = 0u;
             D.obs = (S.lane == 0) ? 1000u : ((S.lane == 1) ? e_uid(x) : 0u);
             return 1;
         }
         receive_counters(S, R, H, x, false, 0u);
         return 0;
     }
-    const uint32_t tun = p_tunnel(x), rnd = p_round(x);
+    // pings.  NotifyPktRcv hands every ping seen on an overlay node's devices to
+    // its managers, addressed to it or not (packet-routing-gym.cc:254-259); the
+    // packet itself continues to its addressee (IP forwarding).
+    const uint32_t t = p_tunnel(x), rnd = p_round(x);
+    const uint32_t ti = tun ? (uint32_t)S.T->tinfo[t] : 0u;
+    const bool ovl = !tun || S.T->ovi[v] >= 0;
     if (type == T_PFWD) {                                           // ping-forward-packet-manager.cc:94-156
-        float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
-        if (S.lane == 0) S.pbd[l * L.PBK() + (rnd & (L.PBK() - 1))] = delay;
-        if (!link_send(S, R, H, (uint32_t)S.T->lrev[l], p_make(T_PBACK, tun, rnd))) CNT_ADD(S, ctrl_dropped, 1u);
+        const uint32_t tgt = tun ? ti_tgt(ti) : v;
+        if (ovl) {
+            // responder position on the tunnel: its own delay slot
+            const uint32_t pos = tun ? (route(S, ti_org(ti), v) >> 8) - 1u : 0u;
+            const float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
+            if (S.lane == 0) S.pbd[(t * L.PLEN() + pos) * L.PBK() + (rnd & (L.PBK() - 1))] = delay;
+            if (!link_send(S, R, H, (uint32_t)S.T->lrev[l], p_make(T_PBACK, t, pos, rnd))) CNT_ADD(S, ctrl_dropped, 1u);
+        }
+        if (tgt != v) { ctrl_forward(S, R, H, v, tgt, x); return 0; }
     } else {                                                        // ping-back-packet-manager.cc:120-144
-        const uint32_t lt = (uint32_t)S.T->rowptr[v] + tun;
-        const float delay = __uint_as_float(u_ld32((const uint32_t*)S.pbd + lt * L.PBK() + (rnd & (L.PBK() - 1))));
-        int32_t acked = (int32_t)R.pm_ack.get(lt), hole = (int32_t)R.pm_hole.get(lt);
-        int32_t idx = (int32_t)rnd;
-        if (idx <= acked) {
-            fail(H, PRISMA_EBIT_ACKORDER);
-        } else {
-            if (idx > acked + 1 && hole < 0) {
-                R.pm_hole.set(lt, (uint32_t)(acked + 1));
-                uint64_t hd = __double_as_longlong(ping_send_s(L, acked + 1));
-                R.hd_lo.set(lt, (uint32_t)hd);
-                R.hd_hi.set(lt, (uint32_t)(hd >> 32));
-            }
-            R.pm_ack.set(lt, (uint32_t)idx);
-            uint64_t nd = __double_as_longlong(ping_send_s(L, (int64_t)idx + 1));
-            R.nd_lo.set(lt, (uint32_t)nd);
-            R.nd_hi.set(lt, (uint32_t)(nd >> 32));
+        const uint32_t org = tun ? ti_org(ti) : v;
+        if (ovl) {
+            const uint32_t pos = p_pos(x);
+            const float delay = __uint_as_float(
+                u_ld32((const uint32_t*)S.pbd + (t * L.PLEN() + pos) * L.PBK() + (rnd & (L.PBK() - 1))));
+            // the ORIGIN's tunnel index applied to this node's own tunnel list
+            const uint32_t idx = t - (uint32_t)S.T->ovrow[org];
+            const uint32_t v0 = (uint32_t)S.T->ovrow[v];
+            if (idx >= (uint32_t)S.T->ovrow[v + 1] - v0) fail(H, PRISMA_EBIT_PINGIDX);
+            else ping_ack(S, R, H, v0 + idx, rnd, delay);
         }
-        uint32_t MA = L.ma();
-        uint32_t pw = R.pm_win.get(lt);
-        uint32_t wn = pw & 0xffffu, wh = pw >> 16, slot;
-        if (wn >= MA) {
-            slot = wh;
-            wh = (wh + 1 == MA) ? 0 : wh + 1;
-        } else {
-            slot = wh + wn;
-            if (slot >= MA) slot -= MA;
-            wn++;
-        }
-        R.pm_win.set(lt, wn | (wh << 16));
-        if (S.lane == 0) S.win[lt * MA + slot] = delay;
-        // refresh the cached window mean (data-packet-manager.cc:55-65), summed oldest first
-        double sum = 0.0;
-        uint32_t i = wh;
-        for (uint32_t j = 0; j < wn; ++j) {
-            float w = (i == slot) ? delay : __uint_as_float(u_ld32((const uint32_t*)S.win + lt * MA + i));
-            sum += (double)w;
-            i = (i + 1 == MA) ? 0 : i + 1;
-        }
-        uint64_t avg = __double_as_longlong(sum / (double)wn);
-        R.pav_lo.set(lt, (uint32_t)avg);
-        R.pav_hi.set(lt, (uint32_t)(avg >> 32));
+        if (org != v) { ctrl_forward(S, R, H, v, org, x); return 0; }
     }
     receive_counters(S, R, H, x, false, 0u);
     return 0;
@@ -968,11 +1089,10 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
         R.lk_t.v[j] = 0; R.lk_seq.v[j] = 0xffffffffu; R.lk_kind.v[j] = 0;
         R.cp_t.v[j] = 0; R.cp_seq.v[j] = 0; R.wh_t.v[j] = 0; R.wh_seq.v[j] = 0;
         R.p0.v[j] = 0; R.p1.v[j] = 0; R.p2.v[j] = 0; R.qb.v[j] = 0;
-        R.pm_ack.v[j] = 0xffffffffu; R.pm_hole.v[j] = 0xffffffffu; R.pm_win.v[j] = 0;
+        R.pm_lo.v[j] = 0; R.pm_mlo.v[j] = 0; R.pm_mhi.v[j] = 0; R.pm_win.v[j] = 0;
         R.pav_lo.v[j] = 0; R.pav_hi.v[j] = 0;
-        uint64_t nd = __double_as_longlong(ping_send_s(L, 0));
-        R.nd_lo.v[j] = (uint32_t)nd; R.nd_hi.v[j] = (uint32_t)(nd >> 32);
-        R.hd_lo.v[j] = 0; R.hd_hi.v[j] = 0;
+        uint64_t od = __double_as_longlong(ping_send_s(L, 0));
+        R.od_lo.v[j] = (uint32_t)od; R.od_hi.v[j] = (uint32_t)(od >> 32);
     }
     H.now = 0;
     H.ping_t = L.ping_period();                                       // data-packet-manager.cc:118-121
@@ -1219,7 +1339,7 @@ prisma_step_kernel_t(KParams P) {
     if (H.pend && !H.over) {
         if (table_mode) {
             uint32_t pn = u_ld32(&S.h->pend_node), pd = u_ld32(&S.h->pend_ent[1]);
-            const int a = mlp_mode ? mlp_action(S, pn, pd, (lane < L.W()) ? S.obs[lane] : 0u)
+            const int a = mlp_mode ? mlp_action(S, pn, (lane < L.W()) ? S.obs[lane] : 0u)
                                    : (int)rfl((uint32_t)S.table[pn * NN + pd]);
             H.hops_launch += finish_pending(S, R, H, a);
         } else if (P.actions) {
@@ -1267,11 +1387,11 @@ prisma_step_kernel_t(KParams P) {
             TM_MARK(1);
             if (need) {
                 if (table_mode) {
-                    const int a = mlp_mode ? mlp_action(S, D.v, D.dst, D.obs)
+                    const int a = mlp_mode ? mlp_action(S, D.v, D.obs)
                                            : (int)rfl((uint32_t)S.table[D.v * NN + D.dst]);
                     apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, a, true,
                                    D.reward, D.prev, D.obs,
-                                   (D.flags & PEND_ECHO) ? (uint32_t)S.T->lrev[id] : kNoLink);
+                                   (D.flags & PEND_ECHO) ? (uint32_t)S.T->lrev[id] : kNoLink, D.last, D.ttl);
                     H.hops_launch++;
                     if (H.hops_launch >= max_hops) H.stop = 1;
                     TM_MARK(2);
@@ -1280,7 +1400,7 @@ prisma_step_kernel_t(KParams P) {
                         Hdr& h = *S.h;
                         h.pend_link = id; h.pend_node = D.v; h.pend_dec = D.d;
                         h.pend_ent[0] = D.x; h.pend_ent[1] = D.dst; h.pend_ent[2] = D.start; h.pend_ent[3] = D.flags;
-                        h.pend_uid = D.uid;
+                        h.pend_uid = D.uid; h.pend_last = D.last;
                     }
                     if (lane < L.W()) S.obs[lane] = D.obs;
                     H.pend = 1;
@@ -1391,6 +1511,129 @@ extern "C" const char* prisma_last_error(void) { return g_err.c_str(); }
 static uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
 static uint32_t next_pow2(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
 
+// Overlay of a topology (host): tunnels, routing, control-packet load per link.
+struct OverlayPlan {
+    bool tunnels = false;                // false: identity overlay (tunnel t == link t)
+    int T = 0, NO = 0, maxdeg = 0, plen = 1, ctrl_max = 2, echo_max = 1;
+    std::vector<int32_t> ovrow, ovi, ovnode;
+    std::vector<uint32_t> tinfo, route;  // route: [N][N] next link | hops << 8
+};
+
+// ns-3 global routing restated for unit link metrics: the SPF
+// pops equal-distance candidates first-in-first-out and scans link records in
+// device order (ascending neighbour id), and without RandomEcmpRouting the
+// first root exit direction is used -- so x forwards towards y through the
+// lowest-id neighbour that lies on a shortest path.  Identical rule in
+// prisma_amd/topology.py:route_tables (the oracle's routing).
+static int plan_overlay(const prisma_topology_t* T, OverlayPlan& OP) {
+    const int N = T->n_nodes, E = T->n_links;
+    std::vector<int32_t> adj((size_t)N * N, -1);             // link id u -> v
+    for (int u = 0; u < N; ++u)
+        for (int l = T->row_ptr[u]; l < T->row_ptr[u + 1]; ++l) adj[(size_t)u * N + T->link_dst[l]] = l;
+    std::vector<int32_t> dist((size_t)N * N, -1);
+    for (int y = 0; y < N; ++y) {
+        std::vector<int> fr(1, y), nx;
+        dist[(size_t)y * N + y] = 0;
+        while (!fr.empty()) {
+            nx.clear();
+            for (int u : fr)
+                for (int l = T->row_ptr[u]; l < T->row_ptr[u + 1]; ++l) {
+                    const int w = T->link_dst[l];
+                    if (dist[(size_t)w * N + y] < 0) { dist[(size_t)w * N + y] = dist[(size_t)u * N + y] + 1; nx.push_back(w); }
+                }
+            fr.swap(nx);
+        }
+    }
+    for (size_t i = 0; i < dist.size(); ++i)
+        if (dist[i] < 0) return set_err(PRISMA_ERR_CONFIG, "the physical topology must be connected");
+    std::vector<int32_t> hop((size_t)N * N, -1);
+    for (int x = 0; x < N; ++x)
+        for (int y = 0; y < N; ++y) {
+            if (x == y) continue;
+            for (int l = T->row_ptr[x]; l < T->row_ptr[x + 1]; ++l)   // ascending neighbour id
+                if (dist[(size_t)T->link_dst[l] * N + y] == dist[(size_t)x * N + y] - 1) { hop[(size_t)x * N + y] = l; break; }
+        }
+    // overlay nodes and adjacency
+    const int NO = T->n_overlay > 0 ? T->n_overlay : N;
+    if (NO < 2 || NO > N) return set_err(PRISMA_ERR_CONFIG, "n_overlay must be 0 or in [2, n_nodes]");
+    if (T->n_overlay > 0 && (!T->overlay_nodes || !T->overlay_adj)) return set_err(PRISMA_ERR_ARG, "null overlay array");
+    OP.NO = NO;
+    OP.ovi.assign(N, -1);
+    OP.ovnode.resize(NO);
+    for (int i = 0; i < NO; ++i) {
+        const int u = T->n_overlay > 0 ? T->overlay_nodes[i] : i;
+        if (u < 0 || u >= N || OP.ovi[u] >= 0) return set_err(PRISMA_ERR_CONFIG, "bad overlay_nodes");
+        OP.ovi[u] = i;
+        OP.ovnode[i] = u;
+    }
+    auto oadj = [&](int i, int j) -> bool {
+        return T->n_overlay > 0 ? T->overlay_adj[(size_t)i * NO + j] != 0 : adj[(size_t)i * N + j] >= 0;
+    };
+    for (int i = 0; i < NO; ++i)
+        for (int j = 0; j < NO; ++j)
+            if (oadj(i, j) != oadj(j, i) || (i == j && oadj(i, i)))
+                return set_err(PRISMA_ERR_CONFIG, "overlay adjacency must be symmetric without self-loops");
+    // tunnels grouped by underlay id, each node's in ascending overlay index (sim.cc:469-476)
+    OP.ovrow.assign(N + 1, 0);
+    std::vector<int> tsrc, tdst;
+    for (int u = 0; u < N; ++u) {
+        const int i = OP.ovi[u];
+        int deg = 0;
+        if (i >= 0)
+            for (int j = 0; j < NO; ++j)
+                if (oadj(i, j)) { tsrc.push_back(u); tdst.push_back(OP.ovnode[j]); ++deg; }
+        if (i >= 0 && deg == 0) return set_err(PRISMA_ERR_CONFIG, "an overlay node has no overlay neighbour");
+        OP.maxdeg = deg > OP.maxdeg ? deg : OP.maxdeg;
+        OP.ovrow[u + 1] = (int32_t)tsrc.size();
+    }
+    OP.T = (int)tsrc.size();
+    if (OP.T > 256) return set_err(PRISMA_ERR_CONFIG, "more than 256 tunnels (8-bit tunnel ids)");
+    bool ident = (NO == N);
+    for (int t = 0; t < OP.T && ident; ++t) ident = (dist[(size_t)tsrc[t] * N + tdst[t]] == 1);
+    for (int i = 0; i < NO && ident; ++i) ident = (OP.ovnode[i] == i);
+    OP.tunnels = !ident;
+    OP.tinfo.resize(OP.T);
+    std::vector<int> c_ping(E, 0), c_echo(E, 0);
+    auto walk = [&](int x, int y, std::vector<int>& cnt) {   // count links of the route x -> y
+        while (x != y) { const int l = hop[(size_t)x * N + y]; cnt[l]++; x = T->link_dst[l]; }
+    };
+    for (int t = 0; t < OP.T; ++t) {
+        const int u = tsrc[t], w = tdst[t];
+        const int len = dist[(size_t)u * N + w];
+        if (len > 8) return set_err(PRISMA_ERR_CONFIG, "tunnel longer than 8 links (3-bit responder position)");
+        OP.plen = len > OP.plen ? len : OP.plen;
+        const int l0 = ident ? t : hop[(size_t)u * N + w];
+        OP.tinfo[t] = (uint32_t)l0 | ((uint32_t)w << 8) | ((uint32_t)u << 16) | ((uint32_t)len << 24);
+        // forward path of the pings; a ping-back from every overlay node on it
+        // (reverse of the arrival link, then routed to the origin); the --train
+        // echo from the target likewise
+        walk(u, w, c_ping);
+        int x = u;
+        while (x != w) {
+            const int l = hop[(size_t)x * N + w], nxt = T->link_dst[l];
+            if (OP.ovi[nxt] >= 0) {
+                c_ping[T->link_rev[l]]++;
+                walk(x, u, c_ping);
+                if (nxt == w) { c_echo[T->link_rev[l]]++; walk(x, u, c_echo); }
+            }
+            x = nxt;
+        }
+    }
+    OP.ctrl_max = 2; OP.echo_max = 1;
+    for (int l = 0; l < E; ++l) {
+        OP.ctrl_max = c_ping[l] > OP.ctrl_max ? c_ping[l] : OP.ctrl_max;
+        OP.echo_max = c_echo[l] > OP.echo_max ? c_echo[l] : OP.echo_max;
+    }
+    if (OP.tunnels) {
+        OP.route.assign((size_t)N * N, 0u);
+        for (int x = 0; x < N; ++x)
+            for (int y = 0; y < N; ++y)
+                OP.route[(size_t)x * N + y] = (x == y ? 255u : (uint32_t)hop[(size_t)x * N + y]) |
+                                              ((uint32_t)dist[(size_t)x * N + y] << 8);
+    }
+    return PRISMA_OK;
+}
+
 static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, Layout& L,
                         std::vector<unsigned char>& topo) {
     const int N = T->n_nodes, E = T->n_links, F = T->n_flows;
@@ -1412,27 +1655,35 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
                 return set_err(PRISMA_ERR_CONFIG, "bad link_rev");
         }
     }
-    if (maxdeg != T->max_deg) return set_err(PRISMA_ERR_CONFIG, "max_deg mismatch");
-    if (maxdeg > 127) return set_err(PRISMA_ERR_CONFIG, "degree above 127");
+    (void)maxdeg;
+    // ---- overlay: tunnels along ns-3 global routing (sim.cc:455-476, 683)
+    OverlayPlan OP;
+    int rc = plan_overlay(T, OP);
+    if (rc) return rc;
+    if (OP.maxdeg != T->max_deg) return set_err(PRISMA_ERR_CONFIG, "max_deg mismatch (largest overlay degree)");
+    if (OP.maxdeg > 127) return set_err(PRISMA_ERR_CONFIG, "degree above 127");
     for (int f = 0; f < F; ++f) {
         if (T->flow_src[f] < 0 || T->flow_src[f] >= N || T->flow_dst[f] < 0 || T->flow_dst[f] >= N ||
-            T->flow_src[f] == T->flow_dst[f] || T->flow_rate_bps[f] == 0)
-            return set_err(PRISMA_ERR_CONFIG, "bad flow");
+            T->flow_src[f] == T->flow_dst[f] || T->flow_rate_bps[f] == 0 ||
+            OP.ovi[T->flow_src[f]] < 0 || OP.ovi[T->flow_dst[f]] < 0)
+            return set_err(PRISMA_ERR_CONFIG, "bad flow (flows run between overlay nodes)");
     }
+    const int maxdeg_o = OP.maxdeg;
     if (P->link_bps == 0 || P->link_delay_ns < 0 || P->max_buffer_bytes == 0 || P->packet_size == 0 ||
         P->ma_size == 0 || P->ma_size > 64 || !(P->ping_interval_s > 0.0f))
         return set_err(PRISMA_ERR_CONFIG, "bad link / ping parameters");
     if (!(P->sim_time_s > 0.0) || P->sim_time_s > 4095.0)
         return set_err(PRISMA_ERR_CONFIG, "sim_time_s must be in (0, 4095] (12-bit packet start second)");
-    if (P->sim_time_s / (double)P->ping_interval_s >= (double)(1u << 21))
-        return set_err(PRISMA_ERR_CONFIG, "more than 2^21 ping rounds per episode (21-bit round index)");
+    if (P->sim_time_s / (double)P->ping_interval_s >= (double)(1u << 17))
+        return set_err(PRISMA_ERR_CONFIG, "more than 2^17 ping rounds per episode (18-bit round field)");
     if (P->log_capacity < 1024 || P->log_capacity > (1u << 22) || (P->log_capacity & (P->log_capacity - 1)))
         return set_err(PRISMA_ERR_CONFIG, "log_capacity must be a power of two >= 1024");
 
     memset(&L, 0, sizeof(L));
     const int Lk = E + N;
-    L.N = N; L.E = E; L.L = Lk; L.F = F; L.max_deg = maxdeg;
-    L.W = (1 + maxdeg + 3) & ~3;                    // obs width: multiple of 4 (16-B record rows)
+    L.N = N; L.E = E; L.L = Lk; L.F = F; L.max_deg = maxdeg_o;
+    L.T = OP.T; L.NO = OP.NO; L.tunnels = OP.tunnels ? 1u : 0u; L.PLEN = (uint32_t)OP.plen;
+    L.W = (1 + maxdeg_o + 3) & ~3;                  // obs width: multiple of 4 (16-B record rows)
     L.MA = (int)P->ma_size;
     L.data_size = P->packet_size + 30u;             // UDP 8 + IP 20 + PPP 2
     L.ping_size = 8u + 30u;
@@ -1462,23 +1713,25 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.WCAP = (int)next_pow2(wire < 2 ? 2 : wire);
     if (L.WCAP > 64) return set_err(PRISMA_ERR_CONFIG, "propagation delay too long for the wire model");
     // ring capacity: full byte-limited FIFO of data + the control packets that
-    // can be queued at once (<= 2 pings per round over the FIFO's drain time)
+    // can be queued at once: per round, the pings and ping-backs whose route
+    // crosses the link (2 on identity overlays), over the time a ping can spend
+    // on its round trip (2 * tunnel length FIFOs and wires)
     double drain_s = (double)P->max_buffer_bytes * 8.0 / (double)P->link_bps + (double)L.sw_txd * 1e-9;
-    double span = 2.0 * drain_s + 2.0 * (double)P->link_delay_ns * 1e-9;
-    uint32_t ctrl = 2u * ((uint32_t)(span / (double)P->ping_interval_s) + 3u);
-    // --train echoes on a link answer data packets that crossed the reverse link,
-    // which arrive at least one data transmission apart: at most drain/tx_data + 2
-    // of them wait in a FIFO at once
-    uint32_t echoes = L.train ? (uint32_t)(drain_s / ((double)L.sw_txd * 1e-9)) + 2u : 0u;
+    double span = 2.0 * (double)OP.plen * (drain_s + (double)P->link_delay_ns * 1e-9);
+    uint32_t ctrl = (uint32_t)OP.ctrl_max * ((uint32_t)(span / (double)P->ping_interval_s) + 3u);
+    // --train echoes on a link answer data packets that crossed a tunnel whose
+    // echo route uses the link; per tunnel they arrive at least one data
+    // transmission apart: at most drain/tx_data + 2 of them wait in a FIFO at once
+    uint32_t echoes = L.train ? (uint32_t)OP.echo_max * ((uint32_t)(drain_s / ((double)L.sw_txd * 1e-9)) + 2u) : 0u;
     uint32_t qs = P->max_buffer_bytes / L.data_size + ctrl + echoes + (uint32_t)L.WCAP;
     qs = (qs + (uint32_t)L.WCAP - 1) / (uint32_t)L.WCAP * (uint32_t)L.WCAP;
     if (qs > 65535u) return set_err(PRISMA_ERR_CONFIG, "queue too deep");
     L.qcap_s = qs;
     L.qcap_a = (uint32_t)(L.WCAP < 8 ? 8 : L.WCAP);
     uint32_t tot = (uint32_t)E * L.qcap_s + (uint32_t)N * L.qcap_a;
-    // ping-back delay slots per tunnel: round k's slot is reused by round
-    // k + PBK, whose forward ping arrives after round k's ping-back (at most
-    // span after k's send) has been consumed
+    // ping-back delay slots per (tunnel, responder): round k's slot is reused
+    // by round k + PBK, whose forward ping arrives after round k's ping-back
+    // (at most span after k's send) has been consumed
     L.PBK = next_pow2((uint32_t)(span / (double)P->ping_interval_s) + 2u);
     // wire arrival times are kept as their low 32 bits relative to the clock
     int64_t max_acc = 0;
@@ -1490,9 +1743,9 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     uint32_t o = 0;
     auto take = [&](uint32_t bytes) { uint32_t r = o; o = align16(o + bytes); return r; };
     L.table_bytes = (uint32_t)(N * N);
-    L.topo_bytes = (uint32_t)sizeof(TopoImage);
-    if (Lk > 256 || E > 256 || F > 512) return set_err(PRISMA_ERR_CONFIG, "topology image limits exceeded");
-    topo.assign(sizeof(TopoImage), 0);
+    L.topo_bytes = (uint32_t)sizeof(TopoImage) + (OP.tunnels ? 4u * (uint32_t)(N * N) : 0u);
+    if (Lk > 256 || E > 256 || F > 512 || OP.T > 256) return set_err(PRISMA_ERR_CONFIG, "topology image limits exceeded");
+    topo.assign(L.topo_bytes, 0);
     TopoImage& TI = *(TopoImage*)topo.data();
     memcpy(TI.rowptr, T->row_ptr, 4u * (N + 1));
     memcpy(TI.ldst, ldst.data(), 4u * Lk);
@@ -1502,13 +1755,19 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     memcpy(TI.fdst, T->flow_dst, 4u * F);
     for (int f = 0; f < F; ++f)                      // poisson-application.cc:280-283
         TI.fmean[f] = (double)(P->packet_size * 8u) / (double)T->flow_rate_bps[f];
+    memcpy(TI.ovrow, OP.ovrow.data(), 4u * (N + 1));
+    memcpy(TI.tinfo, OP.tinfo.data(), 4u * OP.T);
+    for (int x = 0; x < N; ++x) TI.ovi[x] = OP.ovi[x];
+    memcpy(TI.ovnode, OP.ovnode.data(), 4u * OP.NO);
+    if (OP.tunnels) memcpy(topo.data() + sizeof(TopoImage), OP.route.data(), 4u * (size_t)N * N);
 
     // state image: LDS part (staged into LDS) then register part (staged into VGPRs)
     int fs = 1, ls = 1;
     while (64 * fs < F) fs *= 2;
-    while (64 * ls < Lk) ls *= 2;
+    while (64 * ls < (Lk > OP.T ? Lk : OP.T)) ls *= 2;
     if (fs > 8 || ls > 4)
-        return set_err(PRISMA_ERR_CONFIG, "more than 512 flows or 256 links per replica (register-resident engine)");
+        return set_err(PRISMA_ERR_CONFIG,
+                       "more than 512 flows or 256 links / tunnels per replica (register-resident engine)");
     L.FS = fs; L.LS = ls;
     o = 0;
     L.s_hdr = take(sizeof(Hdr));
@@ -1519,10 +1778,10 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.s_wt = take(4u * Lk * L.WCAP);
     L.s_wseq = take(4u * Lk * L.WCAP);
     L.s_ring = take(4u * tot);
-    L.s_win = take(4u * E * L.MA);
-    L.s_pbd = take(4u * E * L.PBK);
+    L.s_win = take(4u * (uint32_t)OP.T * L.MA);
+    L.s_pbd = take(4u * (uint32_t)OP.T * L.PLEN * L.PBK);
     L.lds_state_bytes = o;
-    L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 20u * 64u * (uint32_t)ls));
+    L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 19u * 64u * (uint32_t)ls));
     L.state_bytes = o;
     L.lds_bytes = L.lds_state_bytes + align16(L.table_bytes);
     L.s_mlp = L.lds_bytes;                          // + 256 B of DQN-buffer activations (MLP launches only)

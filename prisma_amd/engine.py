@@ -35,6 +35,7 @@ class _Topo(C.Structure):
         ("n_nodes", C.c_int32), ("n_links", C.c_int32), ("n_flows", C.c_int32), ("max_deg", C.c_int32),
         ("row_ptr", C.c_void_p), ("link_dst", C.c_void_p), ("link_rev", C.c_void_p),
         ("flow_src", C.c_void_p), ("flow_dst", C.c_void_p), ("flow_rate_bps", C.c_void_p),
+        ("n_overlay", C.c_int32), ("overlay_nodes", C.c_void_p), ("overlay_adj", C.c_void_p),
     ]
 
 
@@ -107,7 +108,7 @@ def load_library(path: str = None):
     L.prisma_plan.argtypes = [C.POINTER(_Topo), C.POINTER(_Params), C.POINTER(_Plan)]
     L.prisma_destroy.restype = None
     L.prisma_destroy.argtypes = [C.c_void_p]
-    if L.prisma_abi_version() != 4:
+    if L.prisma_abi_version() != 5:
         raise PrismaError("libprisma_amd ABI version mismatch")
     _lib = L
     return L
@@ -134,6 +135,13 @@ def _topo_struct(topo: Topology):
             np.ascontiguousarray(topo.flow_dst, dtype=np.int32),
             np.ascontiguousarray(topo.flow_rate_bps, dtype=np.uint64)]
     t = _Topo(topo.n_nodes, topo.n_links, topo.n_flows, topo.max_deg, *[a.ctypes.data for a in keep])
+    if not topo.identity:                      # identity overlays pass n_overlay = 0
+        ov = [np.ascontiguousarray(topo.overlay_nodes, dtype=np.int32),
+              np.ascontiguousarray(topo.overlay_adj, dtype=np.int32)]
+        keep += ov
+        t.n_overlay = topo.n_overlay
+        t.overlay_nodes = ov[0].ctypes.data
+        t.overlay_adj = ov[1].ctypes.data
     return t, keep
 
 

@@ -54,7 +54,7 @@ def decode_records(rec: torch.Tensor, W: int) -> dict:
     return {
         "t_ns": i64[:, 0], "uid": i32[:, 2], "prev": i32[:, 3], "reward": f64[:, 2],
         "node": nd & 0xFF, "dst": (nd >> 8) & 0xFF, "start_s": (nd >> 16) & 0xFFFF, "action": act,
-        "status": (w7 >> 8) & 0xFF, "episode": (w7 >> 16) & 0xFFFF, "obs": i32[:, 8:8 + W],
+        "status": (w7 >> 8) & 0xFF, "ttl": (w7 >> 16) & 0xFF, "episode": (w7 >> 24) & 0xFF, "obs": i32[:, 8:8 + W],
     }
 
 

@@ -15,7 +15,9 @@
   greedy (train=0, forwarder.py:183-186).
 
 One network per overlay node (the reference's per-node agents), stored
-stacked over nodes with the action/input dimension padded to max_deg so a
+stacked over UNDERLAY node ids (rows of non-overlay nodes stay zero; the one-hot
+input is obs[0], the destination's overlay index, so W1 rows past N_o are
+unused), with the action/input dimension padded to max_deg so a
 whole batch of decisions at different nodes is ONE set of batched GEMMs
 (torch.bmm over the gathered per-node weights), not a Python loop over nodes.
 """
@@ -31,12 +33,17 @@ from .topology import Topology, sp_next_hop_table
 
 
 class SPPolicy:
+    """obs[0] is the destination's overlay index (data-packet-manager.cc:175); the table
+    is indexed by underlay ids (node, destination)."""
+
     def __init__(self, topo: Topology, device="cuda"):
         self.topo = topo
         self.table = torch.from_numpy(sp_next_hop_table(topo)).to(device)
+        self.dst_of = torch.from_numpy(topo.overlay_nodes.astype(np.int64)).to(device)
 
     def act(self, obs: torch.Tensor, node: torch.Tensor) -> torch.Tensor:
-        return self.table[node.long(), obs[:, 0].long()].to(torch.int32)
+        dst = self.dst_of[obs[:, 0].long().clamp(0, self.dst_of.numel() - 1)]
+        return self.table[node.long(), dst].to(torch.int32)
 
 
 def _he_uniform(gen: torch.Generator, fan_in: int, shape) -> torch.Tensor:
@@ -53,6 +60,7 @@ class StackedQNet(torch.nn.Module):
             raise ValueError("kind must be 'routing' or 'buffer'")
         self.kind = kind
         self.N = topo.n_nodes
+        self.topo_overlay_nodes = topo.overlay_nodes.astype(np.int64)
         self.D = topo.max_deg
         deg = torch.from_numpy(topo.degrees.astype(np.int64))
         self.register_buffer("deg", deg)
@@ -66,11 +74,13 @@ class StackedQNet(torch.nn.Module):
             for u in range(N):
                 fi = int(fan_ins[u])
                 do = int(dout[u]) if not isinstance(dout, int) else dout
+                if int(topo.degrees[u]) == 0:
+                    continue                                  # not an overlay node: no agent
                 W[u, :fi, :do] = _he_uniform(g, fi, (fi, do))
                 b[u, :do] = _he_uniform(g, do, (do,))
             return torch.nn.Parameter(W), torch.nn.Parameter(b)
 
-        ones = [N] * N
+        ones = [topo.n_overlay] * N                                 # one_hot(dst, numNodes)
         self.W1, self.b1 = dense(ones, N, 32)                       # one-hot(dst) branch
         if kind == "buffer":
             self.Wb, self.bb = dense(topo.degrees, D, 32)           # buffers branch (deg inputs)
@@ -127,14 +137,20 @@ class StackedQNet(torch.nn.Module):
 
     @torch.no_grad()
     def argmin_table(self) -> torch.Tensor:
-        """[N, N] uint8 action table (valid for kind='routing': Q depends on (node, dst) only)."""
+        """[N, N] uint8 action table by underlay ids (node, destination); valid for
+        kind='routing' (Q depends on (node, dst) only).  Rows / columns of non-overlay
+        nodes are 0."""
         if self.kind != "routing":
             raise ValueError("only the DQ-routing model has a state-independent argmin table")
         dev = self.W1.device
-        node = torch.arange(self.N, device=dev).repeat_interleave(self.N)
-        dst = torch.arange(self.N, device=dev).repeat(self.N)
-        obs = torch.zeros((self.N * self.N, 1 + self.D), dtype=torch.int32, device=dev)
-        obs[:, 0] = dst.to(torch.int32)
-        a = self.act(obs, node).view(self.N, self.N)
+        on = torch.from_numpy(self.topo_overlay_nodes).to(dev)
+        no = on.numel()
+        node = on.repeat_interleave(no)
+        dsti = torch.arange(no, device=dev).repeat(no)
+        obs = torch.zeros((no * no, 1 + self.D), dtype=torch.int32, device=dev)
+        obs[:, 0] = dsti.to(torch.int32)
+        a = self.act(obs, node).view(no, no)
         a.fill_diagonal_(0)                                   # at destination: action 0 (forwarder.py:149)
-        return a.to(torch.uint8)
+        table = torch.zeros((self.N, self.N), dtype=torch.uint8, device=dev)
+        table[on[:, None], on[None, :]] = a.to(torch.uint8)
+        return table

@@ -5,7 +5,7 @@ import numpy as np
 
 ST_PENDING, ST_ENQUEUED, ST_DROPPED, ST_DESTINATION, ST_DISCARDED = 0, 1, 2, 3, 4
 
-EBIT_RING, EBIT_WIRE, EBIT_ACKORDER, EBIT_TIME, EBIT_LOGWRAP = 1, 2, 4, 8, 16
+EBIT_RING, EBIT_WIRE, EBIT_ACKORDER, EBIT_TIME, EBIT_LOGWRAP, EBIT_PINGIDX = 1, 2, 4, 8, 16, 32
 
 
 def record_dtype(obs_width: int) -> np.dtype:
@@ -15,7 +15,7 @@ def record_dtype(obs_width: int) -> np.dtype:
     return np.dtype([
         ("t_ns", "<i8"), ("uid", "<u4"), ("prev", "<i4"), ("reward", "<f8"),
         ("node", "u1"), ("dst", "u1"), ("start_s", "<u2"), ("action", "i1"), ("status", "u1"),
-        ("episode", "<u2"), ("obs", "<u4", (obs_width,)),
+        ("ttl", "u1"), ("episode", "u1"), ("obs", "<u4", (obs_width,)),
     ])
 
 
@@ -29,8 +29,9 @@ COUNTERS_DTYPE = np.dtype([
     ("episode", "<u4"), ("ping_rounds", "<u4"), ("seq", "<u4"), ("uid", "<u4"),
     ("dec_count", "<u4"), ("ctrl_dropped", "<u4"), ("error", "<u4"), ("episode_over", "<u4"),
     ("hops_total", "<u8"), ("events_total", "<u8"),
+    ("un_cost_sum", "<f4"), ("un_cost_n", "<i4"),
 ])
-assert COUNTERS_DTYPE.itemsize == 144
+assert COUNTERS_DTYPE.itemsize == 152
 
 
 def transitions(records: np.ndarray, loss_penalty: float):

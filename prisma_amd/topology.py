@@ -1,9 +1,7 @@
-"""Scenario construction: topology, links and Poisson flows of one replica.
+"""Scenario construction: topology, links, overlay tunnels and Poisson flows of one replica.
 
-Restates the reference's scenario builder (prisma/ns3/sim.cc) for the
-identity-overlay configurations (every underlay node is an overlay node,
-overlay adjacency == physical adjacency: the shipped abilene and geant
-examples).  Everything here is host-side, run once per environment.
+Restates the reference's scenario builder (prisma/ns3/sim.cc).  Everything
+here is host-side, run once per environment.
 
 Reference behaviour mirrored (file:line relative to the reference root):
   * matrix readers stop at the first empty line and require square
@@ -11,14 +9,27 @@ Reference behaviour mirrored (file:line relative to the reference root):
   * traffic-matrix entries are ns-3 DataRate strings parsed with the
     truncating ns-3 rule ``(uint64_t)(r * multiplier)`` and scaled as
     ``ceil(rate * load_factor)`` (sim.cc:604, 623);
-  * one flow per ordered overlay pair (i != j) with a non-zero parsed rate
-    (sim.cc:494-514, 599-604), created in (i, j) order;
-  * neighbour (action) order is ascending neighbour id (sim.cc:469-476,
-    networkx adjacency order used by forwarder.py:191);
+  * one flow per ordered pair of OVERLAY nodes (i != j, underlay ids, in
+    (i, j) underlay order) with a non-zero parsed rate (sim.cc:494-514,
+    599-604);
+  * the overlay neighbour (action) list of overlay node i is its overlay
+    neighbours in ascending overlay index, stored as underlay ids
+    (sim.cc:469-476); identity overlays give ascending neighbour ids
+    (networkx adjacency order used by forwarder.py:191);
   * the access link host i -> switch i runs at 1e6 * link_cap * deg(i) b/s
-    with zero delay (sim.cc:398-410);
+    (deg = PHYSICAL degree, sim.cc:341-349) with zero delay (sim.cc:398-410);
   * loss_penalty = ((max_buffer + packet_size + 30) * 8 / cap + 0.001) * N
-    (argument_parser.py:163).
+    with N = number of overlay nodes (argument_parser.py:127-128,163).
+
+Tunnelled overlays: an overlay hop u -> w is IP-forwarded
+along the underlay route that ns-3 global routing installs for the host
+10.2.2.(w+1) (sim.cc:683, data-packet-manager.cc:271-287).  With unit link
+metrics, ns-3's SPF (equal-distance candidates popped first-in-first-out,
+link records in device order = ascending neighbour id, first root exit
+direction used when RandomEcmpRouting is off) picks at every node x the
+LOWEST-id neighbour that lies on some shortest path to w; ``route_tables``
+restates that rule (pinned by a hand-checked known answer on the shipped
+overlay_full_mesh_3n_abilene example, tests/test_topology.py).
 """
 from __future__ import annotations
 
@@ -105,12 +116,50 @@ def loss_penalty(max_buffer: int, packet_size: int, link_cap: int, n_nodes: int)
     return ((((max_buffer + packet_size + 30) * 8) / link_cap) + 0.001) * n_nodes
 
 
+def route_tables(adj: np.ndarray):
+    """ns-3 global routing restated for unit metrics (module docstring).
+
+    Returns (next_hop [N, N] int32, dist [N, N] int32): next_hop[x, y] is the
+    neighbour x forwards to for destination y (-1 on the diagonal), the
+    lowest-id neighbour n of x with dist[n, y] == dist[x, y] - 1."""
+    n = adj.shape[0]
+    nb = [[v for v in range(n) if adj[u, v]] for u in range(n)]
+    dist = np.full((n, n), -1, dtype=np.int32)
+    for y in range(n):                      # BFS from every destination
+        dist[y, y] = 0
+        frontier = [y]
+        while frontier:
+            nxt = []
+            for u in frontier:
+                for v in nb[u]:
+                    if dist[v, y] < 0:
+                        dist[v, y] = dist[u, y] + 1
+                        nxt.append(v)
+            frontier = nxt
+    if np.any(dist < 0):
+        raise ValueError("the physical topology must be connected")
+    hop = np.full((n, n), -1, dtype=np.int32)
+    for x in range(n):
+        for y in range(n):
+            if x != y:
+                hop[x, y] = min(v for v in nb[x] if dist[v, y] == dist[x, y] - 1)
+    return hop, dist
+
+
 @dataclass
 class Topology:
-    """One replica's network: CSR links + flow table (host numpy arrays)."""
+    """One replica's network: physical CSR links, overlay tunnels, flow table
+    (host numpy arrays).
+
+    Links (row_ptr/link_dst/link_src/link_rev) are the PHYSICAL directed
+    switch links.  Decisions happen at overlay nodes over TUNNELS: tunnel t
+    of node u = ov_row_ptr[u] + a (a = action index) goes to overlay
+    neighbour tun_dst[t] (underlay id) along next_hop; its first link is
+    tun_link[t] and it crosses tun_len[t] links.  For identity overlays
+    tunnels == links (t == l)."""
 
     n_nodes: int
-    adjacency: np.ndarray            # [N, N] 0/1
+    adjacency: np.ndarray            # [N, N] 0/1 physical
     row_ptr: np.ndarray              # [N+1] int32
     link_dst: np.ndarray             # [E] int32
     link_src: np.ndarray             # [E] int32
@@ -121,7 +170,16 @@ class Topology:
     flow_base_bps: np.ndarray        # [F] uint64 (parsed, before load factor)
     name: str = "custom"
     load_factor: float = 1.0
-    overlay_index: Optional[np.ndarray] = None
+    overlay_index: Optional[np.ndarray] = None     # [N] overlay index of node x, -1 if none
+    overlay_nodes: Optional[np.ndarray] = None     # [N_o] underlay id of overlay node i
+    overlay_adj: Optional[np.ndarray] = None       # [N_o, N_o] 0/1
+    ov_row_ptr: Optional[np.ndarray] = None        # [N+1] tunnels per node (0 for non-overlay)
+    tun_src: Optional[np.ndarray] = None           # [T]
+    tun_dst: Optional[np.ndarray] = None           # [T]
+    tun_link: Optional[np.ndarray] = None          # [T] first physical link
+    tun_len: Optional[np.ndarray] = None           # [T] links crossed
+    next_hop: Optional[np.ndarray] = None          # [N, N] routing (route_tables)
+    dist: Optional[np.ndarray] = None              # [N, N] hop distance
 
     @property
     def n_links(self) -> int:
@@ -132,7 +190,26 @@ class Topology:
         return int(self.flow_src.shape[0])
 
     @property
+    def n_tunnels(self) -> int:
+        return int(self.tun_dst.shape[0])
+
+    @property
+    def n_overlay(self) -> int:
+        return int(self.overlay_nodes.shape[0])
+
+    @property
+    def identity(self) -> bool:
+        """Every node is an overlay node and every tunnel is one link."""
+        return self.n_overlay == self.n_nodes and bool(np.all(self.tun_len == 1)) and \
+            bool(np.array_equal(self.overlay_nodes, np.arange(self.n_nodes)))
+
+    @property
     def degrees(self) -> np.ndarray:
+        """Overlay degree (number of actions) per underlay node, 0 off the overlay."""
+        return np.diff(self.ov_row_ptr).astype(np.int32)
+
+    @property
+    def phys_degrees(self) -> np.ndarray:
         return np.diff(self.row_ptr).astype(np.int32)
 
     @property
@@ -145,16 +222,31 @@ class Topology:
         return (w + 3) & ~3
 
     def neighbors(self, u: int) -> List[int]:
+        """Overlay neighbours of u (underlay ids, action order)."""
+        return [int(x) for x in self.tun_dst[self.ov_row_ptr[u]:self.ov_row_ptr[u + 1]]]
+
+    def phys_neighbors(self, u: int) -> List[int]:
         return [int(x) for x in self.link_dst[self.row_ptr[u]:self.row_ptr[u + 1]]]
 
     def link_id(self, u: int, v: int) -> int:
-        nb = self.neighbors(u)
+        nb = self.phys_neighbors(u)
         return int(self.row_ptr[u]) + nb.index(v)
+
+    def tunnel_path(self, t: int) -> List[int]:
+        """Underlay nodes of tunnel t, origin first."""
+        x, y = int(self.tun_src[t]), int(self.tun_dst[t])
+        path = [x]
+        while x != y:
+            x = int(self.next_hop[x, y])
+            path.append(x)
+        return path
 
     # ------------------------------------------------------------------
     @classmethod
     def from_matrices(cls, adjacency, tm_strings, load_factor: float = 1.0,
-                      name: str = "custom") -> "Topology":
+                      name: str = "custom", map_overlay=None, overlay_adjacency=None) -> "Topology":
+        """map_overlay[x] = overlay index of underlay node x or -1 (map_overlay.txt);
+        default: identity overlay (overlay_adjacency = adjacency)."""
         adj = (np.asarray(adjacency) != 0).astype(np.int32)
         n = adj.shape[0]
         if adj.shape != (n, n):
@@ -166,6 +258,25 @@ class Topology:
         tm = np.asarray(tm_strings, dtype=object)
         if tm.shape != (n, n):
             raise ValueError(f"traffic matrix shape {tm.shape} != ({n}, {n}) (sim.cc:310-313)")
+        if map_overlay is None:
+            mapo = np.arange(n, dtype=np.int64)
+            oadj = adj.copy()
+        else:
+            mapo = np.asarray(map_overlay, dtype=np.int64)
+            oadj = (np.asarray(overlay_adjacency) != 0).astype(np.int32)
+        if mapo.shape != (n,):
+            raise ValueError(f"map_overlay has {mapo.shape[0]} entries for {n} underlay nodes")
+        n_o = int((mapo >= 0).sum())
+        if sorted(int(v) for v in mapo if v >= 0) != list(range(n_o)):
+            raise ValueError("map_overlay must number the overlay nodes 0..N_o-1")
+        if oadj.shape != (n_o, n_o) or np.any(np.diag(oadj)) or not np.array_equal(oadj, oadj.T):
+            raise ValueError("overlay adjacency must be a symmetric N_o x N_o matrix without self-loops")
+        overlay_nodes = np.zeros(n_o, dtype=np.int32)
+        for x in range(n):
+            if mapo[x] >= 0:
+                overlay_nodes[mapo[x]] = x
+        overlay_index = mapo.astype(np.int32)
+
         row_ptr = np.zeros(n + 1, dtype=np.int32)
         dst, src = [], []
         for u in range(n):
@@ -181,11 +292,30 @@ class Topology:
                             dtype=np.int32)
         if np.any(row_ptr[1:] - row_ptr[:-1] == 0):
             raise ValueError("every node needs at least one link")
+        hop, dist = route_tables(adj)
+
+        # tunnels: grouped by underlay id, each node's in ascending overlay index (sim.cc:469-476)
+        ov_row_ptr = np.zeros(n + 1, dtype=np.int32)
+        ts, td = [], []
+        for u in range(n):
+            if mapo[u] >= 0:
+                i = int(mapo[u])
+                nbr = [int(overlay_nodes[j]) for j in range(n_o) if oadj[i, j]]
+                if not nbr:
+                    raise ValueError(f"overlay node {i} has no overlay neighbour")
+                ts.extend([u] * len(nbr))
+                td.extend(nbr)
+            ov_row_ptr[u + 1] = len(td)
+        tun_src = np.array(ts, dtype=np.int32)
+        tun_dst = np.array(td, dtype=np.int32)
+        tun_link = np.array([index[(int(a), int(hop[a, b]))] for a, b in zip(ts, td)], dtype=np.int32)
+        tun_len = np.array([int(dist[a, b]) for a, b in zip(ts, td)], dtype=np.int32)
+
         fs, fd, fr, fb = [], [], [], []
         for i in range(n):
             for j in range(n):
-                if i == j:
-                    continue
+                if i == j or mapo[i] < 0 or mapo[j] < 0:
+                    continue                       # activateUnderlayTraffic=0: overlay pairs only
                 base = parse_data_rate(str(tm[i, j])) if not isinstance(tm[i, j], (int, np.integer)) \
                     else int(tm[i, j])
                 if base <= 0:
@@ -200,7 +330,9 @@ class Topology:
                    flow_rate_bps=np.array(fr, dtype=np.uint64),
                    flow_base_bps=np.array(fb, dtype=np.uint64),
                    name=name, load_factor=float(load_factor),
-                   overlay_index=np.arange(n, dtype=np.int32))
+                   overlay_index=overlay_index, overlay_nodes=overlay_nodes, overlay_adj=oadj,
+                   ov_row_ptr=ov_row_ptr, tun_src=tun_src, tun_dst=tun_dst, tun_link=tun_link,
+                   tun_len=tun_len, next_hop=hop, dist=dist)
 
     @classmethod
     def from_files(cls, physical_adjacency: str, overlay_adjacency: str, map_overlay: str,
@@ -209,14 +341,8 @@ class Topology:
         over = read_square(overlay_adjacency)
         mapo = read_map_overlay(map_overlay)
         tm = read_square(traffic_matrix, kind=str)
-        identity = (phys.shape == over.shape and np.array_equal(phys != 0, over != 0)
-                    and mapo.shape[0] == phys.shape[0]
-                    and np.array_equal(mapo, np.arange(phys.shape[0])))
-        if not identity:
-            raise NotImplementedError(
-                "only identity overlays (map_overlay = 0..N-1, overlay == physical adjacency) are "
-                "supported by this build; tunnelled overlays (SURVEY 8a A15) are a next item")
-        return cls.from_matrices(phys, tm, load_factor=load_factor, name=name)
+        return cls.from_matrices(phys, tm, load_factor=load_factor, name=name,
+                                 map_overlay=mapo, overlay_adjacency=over)
 
     @classmethod
     def example(cls, name: str = "abilene", tm_index: int = 0, load_factor: float = 1.0) -> "Topology":
@@ -286,25 +412,35 @@ def _bidirectional_path(adj_lists: List[List[int]], s: int, t: int) -> List[int]
     return path
 
 
-def sp_next_hop_table(topo: Topology) -> np.ndarray:
-    """[N, N] uint8 action table: index (into neighbors(u)) of the SP next hop.
+def _overlay_lists(topo: Topology) -> List[List[int]]:
+    n_o = topo.n_overlay
+    return [[j for j in range(n_o) if topo.overlay_adj[i, j]] for i in range(n_o)]
 
-    Diagonal entries (packet at its destination) are 0, the action the
-    reference agent sends there (forwarder.py:149-150).
+
+def sp_next_hop_table(topo: Topology) -> np.ndarray:
+    """[N, N] uint8 action table indexed by UNDERLAY ids (node, destination):
+    index (into neighbors(u)) of the SP next hop on the overlay graph G
+    (forwarder.py:190-191 runs nx.shortest_path on the overlay graph, in
+    overlay indices, argument_parser.py:127).
+
+    Diagonal entries (packet at its destination) and rows/columns of
+    non-overlay nodes are 0 (forwarder.py:149-150 sends action 0 there).
     """
     n = topo.n_nodes
-    adj_lists = [topo.neighbors(u) for u in range(n)]
+    lists = _overlay_lists(topo)
+    on = topo.overlay_nodes
     table = np.zeros((n, n), dtype=np.uint8)
-    for u in range(n):
-        for d in range(n):
-            if u == d:
+    for i in range(topo.n_overlay):
+        for j in range(topo.n_overlay):
+            if i == j:
                 continue
-            nxt = _bidirectional_path(adj_lists, u, d)[1]
-            table[u, d] = adj_lists[u].index(nxt)
+            nxt = _bidirectional_path(lists, i, j)[1]
+            table[on[i], on[j]] = lists[i].index(nxt)
     return table
 
 
 def sp_paths(topo: Topology) -> dict:
-    n = topo.n_nodes
-    adj_lists = [topo.neighbors(u) for u in range(n)]
-    return {(u, d): _bidirectional_path(adj_lists, u, d) for u in range(n) for d in range(n) if u != d}
+    """SP paths on the overlay graph, in overlay indices."""
+    lists = _overlay_lists(topo)
+    n_o = topo.n_overlay
+    return {(u, d): _bidirectional_path(lists, u, d) for u in range(n_o) for d in range(n_o) if u != d}

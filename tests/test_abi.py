@@ -32,7 +32,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = engine.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.prisma_abi_version() == 4
+    assert lib.prisma_abi_version() == 5
     out = subprocess.run(["nm", "-D", "--defined-only", engine.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (prisma_\w+)", out))
     assert set(declared_functions()) <= exported
@@ -117,3 +117,18 @@ def test_plan_sizes_and_limits_without_a_device():
     big = Topology.from_matrices(ring, tm)
     with pytest.raises(engine.PrismaError, match="n_nodes"):
         engine.plan(big, engine_params(big))
+
+
+def test_plan_tunnelled_overlay():
+    """overlay_full_mesh_3n_abilene: 12 tunnels over 16 physical links, responder positions
+    up to 2 (two-link tunnels), obs width 1 + 3 -> 4; a non-overlay flow is refused."""
+    from prisma_amd.config import engine_params
+    from prisma_amd.topology import Topology
+    t = Topology.example("overlay_full_mesh_3n_abilene")
+    p = engine.plan(t, engine_params(t))
+    assert p["obs_width"] == 4 and p["record_bytes"] == 48 and p["link_slots"] == 1
+    bad = Topology.example("overlay_full_mesh_3n_abilene")
+    bad.flow_src = bad.flow_src.copy()
+    bad.flow_src[0] = 1                                  # underlay-only node 1
+    with pytest.raises(engine.PrismaError, match="overlay"):
+        engine.plan(bad, engine_params(bad))

@@ -299,3 +299,119 @@ def test_dqn_buffer_in_kernel_parity(oracle_mod, name, ping, train):
     ta = net.act(obs, node).cpu().numpy()
     assert (ta == dec["action"]).mean() > 0.99
     eng.close()
+
+
+# ---- tunnelled overlays ----------------------------------------------
+def _random_table(topo, seed):
+    rng = np.random.default_rng(seed)
+    table = np.zeros((topo.n_nodes, topo.n_nodes), dtype=np.uint8)
+    for u in topo.overlay_nodes:
+        table[u] = rng.integers(0, topo.degrees[u], topo.n_nodes)
+    return table
+
+
+def _ttl_chain():
+    """Underlay path 0-1-2-3-4-5, overlay triangle {0, 3, 5}: tunnel 0<->3 has two
+    intermediate hops and 0->5 crosses overlay node 3 (a ping bystander).  With the
+    bouncing table below a packet for 5 loops 0 <-> 3 until its TTL (255, -2 per loop
+    hop) expires at an intermediate forward."""
+    adj = np.zeros((6, 6), dtype=int)
+    for i in range(5):
+        adj[i, i + 1] = adj[i + 1, i] = 1
+    tm = np.zeros((6, 6), dtype=object)
+    tm[0, 5] = "40Kbps"
+    tm[5, 0] = "20Kbps"
+    tm[3, 0] = "10Kbps"
+    topo = Topology.from_matrices(adj, tm, map_overlay=[0, -1, -1, 1, -1, 2],
+                                  overlay_adjacency=np.ones((3, 3)) - np.eye(3))
+    table = np.zeros((6, 6), dtype=np.uint8)
+    table[0, 5] = 0          # 0 -> 3
+    table[3, 5] = 0          # 3 -> 0
+    table[5, 0] = 1          # 5 -> 3
+    table[3, 0] = 1          # 3 -> 5
+    return topo, table
+
+
+@pytest.mark.parametrize("name,tm,lf,ping,seed,train,pol", [
+    ("overlay_full_mesh_3n_abilene", 0, 1.0, 1, 100, 0, "sp"),
+    ("overlay_full_mesh_3n_abilene", 0, 20.0, 0, 7, 0, "rand"),
+    ("overlay_full_mesh_3n_abilene", 0, 20.0, 1, 9, 1, "rand"),
+    ("abilene_on_geant", 0, 1.0, 1, 100, 0, "sp"),
+    ("abilene_on_geant", 1, 3.0, 0, 5, 1, "rand"),
+    ("abilene_on_geant", 2, 2.0, 1, 8, 0, "rand"),
+])
+def test_tunnel_table_parity(oracle_mod, name, tm, lf, ping, seed, train, pol):
+    topo = Topology.example(name, tm, lf)
+    params = engine_params(topo, sim_time_s=20.0, ping_as_obs=ping, seed=seed, replica_base=2, train=train)
+    table = sp_next_hop_table(topo) if pol == "sp" else _random_table(topo, seed)
+    cnt = run_table_both(oracle_mod, topo, params, 4, 4000, table)
+    if name == "overlay_full_mesh_3n_abilene" and lf > 1:
+        assert cnt["ov_lost"].sum() > 0                   # intermediate and first-link drops
+
+
+def test_tunnel_ttl_expiry_parity(oracle_mod):
+    topo, table = _ttl_chain()
+    params = engine_params(topo, sim_time_s=30.0, ping_as_obs=1)
+    o = oracle_mod.OracleSim(topo, params)
+    o.run_table(table, 10 ** 9)
+    recs = o.records()
+    assert recs["ttl"].min() <= 2                          # packets reach the end of their TTL
+    c = o.counters()
+    assert c["ov_injected"] > c["ov_arrived"] + c["ov_lost"]   # silently expired (never counted)
+    run_table_both(oracle_mod, topo, params, 3, 10 ** 6, table)
+
+
+def test_tunnel_external_notify_train_parity(oracle_mod):
+    topo = Topology.example("overlay_full_mesh_3n_abilene", 0, 10.0)
+    params = engine_params(topo, sim_time_s=4.0, ping_as_obs=1, notify_dest=1, train=1)
+    R = 3
+    eng = PrismaEngine(topo, params, R)
+    eng.reset(0)
+    orcs = [oracle_mod.OracleSim(topo, params, replica=r) for r in range(R)]
+    ref_obs = [o.step(-1) for o in orcs]
+    obs, mask, node = eng.step(None)
+    rng = np.random.default_rng(2)
+    for s in range(1200):
+        g, m, nd = obs.cpu().numpy(), mask.cpu().numpy(), node.cpu().numpy()
+        acts = np.zeros(R, dtype=np.int32)
+        for r in range(R):
+            assert (ref_obs[r] is None) == (m[r] == 0), (s, r)
+            if ref_obs[r] is None:
+                continue
+            assert np.array_equal(ref_obs[r], g[r]), (s, r, g[r], ref_obs[r])
+            assert nd[r] == orcs[r].pending_node()
+            acts[r] = rng.integers(0, topo.degrees[nd[r]])
+        ref_obs = [orcs[r].step(int(acts[r])) if ref_obs[r] is not None else None for r in range(R)]
+        obs, mask, node = eng.step(torch.from_numpy(acts).cuda())
+    torch.cuda.synchronize()
+    cnt = eng.counters()
+    log = eng.log_tensor().cpu().numpy()
+    for r in range(R):
+        ref = orcs[r].records()
+        assert eng.records(r, 0, len(ref), log_host=log).tobytes() == ref.tobytes()
+        assert_counters_equal(cnt[r], orcs[r].counters(), r)
+    eng.close()
+
+
+def test_tunnel_dqn_buffer_parity(oracle_mod):
+    from prisma_amd.policies import StackedQNet
+    topo = Topology.example("abilene_on_geant", 0, 1.0)
+    net = StackedQNet(topo, "buffer", seed=4)
+    w = net.pack()
+    params = engine_params(topo, sim_time_s=10.0, ping_as_obs=1)
+    R, H = 3, 1500
+    eng = PrismaEngine(topo, params, R)
+    eng.reset(0)
+    eng.run(w, H)
+    torch.cuda.synchronize()
+    cnt = eng.counters()
+    log = eng.log_tensor().cpu().numpy()
+    wh = w.cpu().numpy()
+    for r in range(R):
+        o = oracle_mod.OracleSim(topo, params, replica=r)
+        o.run_mlp(wh, H)
+        ref = o.records()
+        assert cnt[r]["error"] == 0
+        assert eng.records(r, 0, len(ref), log_host=log).tobytes() == ref.tobytes(), r
+        assert_counters_equal(cnt[r], o.counters(), r)
+    eng.close()

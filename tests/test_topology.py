@@ -118,10 +118,34 @@ def test_bad_inputs_fail_loudly():
         Topology.from_matrices(np.array([[0, 1], [0, 0]]), [["0bps"] * 2] * 2)  # asymmetric
     with pytest.raises(ValueError):
         Topology.from_matrices(np.array([[0, 1], [1, 0]]), [["0bps"] * 3] * 3)  # TM shape (sim.cc:310)
-    with pytest.raises(NotImplementedError):
-        root = os.path.join(os.path.dirname(os.path.dirname(__file__)), "prisma_amd", "data",
-                            "overlay_full_mesh_3n_abilene")
-        Topology.from_files(f"{root}/topology_files/physical_adjacency_matrix.txt",
-                            f"{root}/topology_files/overlay_adjacency_matrix.txt",
-                            f"{root}/topology_files/map_overlay.txt",
-                            f"{root}/traffic_matrices/node_intensity_normalized_0.txt")
+    with pytest.raises(ValueError):
+        # the shipped overlay example has an 11x11 TM 1 for a 6-node underlay: NS_FATAL_ERROR (sim.cc:310-313)
+        Topology.example("overlay_full_mesh_3n_abilene", 1)
+
+
+def test_overlay_example_tunnels_known_answer():
+    """overlay_full_mesh_3n_abilene (prisma/examples/...): 6-node underlay, overlay nodes
+    0,2,4,5 (map 0 -1 1 -1 2 3), full mesh.  Paths checked by hand against the ns-3 global
+    routing rule (lowest-id neighbour on a shortest path; topology.py docstring):
+    2->4 and 4->2 tie between 1 and 3 and take 1; 0<->5 cross overlay node 2."""
+    t = Topology.example("overlay_full_mesh_3n_abilene")
+    assert t.n_nodes == 6 and t.n_overlay == 4 and not t.identity
+    assert list(t.overlay_nodes) == [0, 2, 4, 5] and list(t.overlay_index) == [0, -1, 1, -1, 2, 3]
+    assert {u: t.neighbors(u) for u in (0, 2, 4, 5)} == {0: [2, 4, 5], 2: [0, 4, 5], 4: [0, 2, 5], 5: [0, 2, 4]}
+    paths = {(int(t.tun_src[k]), int(t.tun_dst[k])): t.tunnel_path(k) for k in range(t.n_tunnels)}
+    assert paths == {(0, 2): [0, 2], (0, 4): [0, 1, 4], (0, 5): [0, 2, 5], (2, 0): [2, 0], (2, 4): [2, 1, 4],
+                     (2, 5): [2, 5], (4, 0): [4, 1, 0], (4, 2): [4, 1, 2], (4, 5): [4, 3, 5], (5, 0): [5, 2, 0],
+                     (5, 2): [5, 2], (5, 4): [5, 3, 4]}
+    assert list(t.tun_len) == [len(paths[(int(a), int(b))]) - 1 for a, b in zip(t.tun_src, t.tun_dst)]
+    # flows only between overlay pairs, underlay (i, j) order (sim.cc:494-514, 599-631)
+    assert list(zip(t.flow_src.tolist(), t.flow_dst.tolist())) == [
+        (0, 2), (0, 4), (0, 5), (2, 0), (2, 4), (2, 5), (4, 0), (4, 2), (4, 5), (5, 0), (5, 2), (5, 4)]
+    assert int(t.flow_rate_bps[7]) == 83                    # "83.85bps" truncates
+    # loss penalty counts overlay nodes (argument_parser.py:127-128,163)
+    assert engine_params(t)["loss_penalty"] == loss_penalty(16260, 512, 500000, 4)
+    # SP agent on the overlay graph (forwarder.py:190-191): full mesh -> direct tunnel
+    table = sp_next_hop_table(t)
+    for u in (0, 2, 4, 5):
+        for d in (0, 2, 4, 5):
+            if u != d:
+                assert t.neighbors(u)[table[u, d]] == d
