@@ -987,7 +987,8 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             reward = (double)py_micros(H.now) / 1e6 - (double)py_micros(t_prev) / 1e6;   // forwarder.py:360
             CNT_ADD(S, reward_sum, reward);
         }
-        const uint32_t o = (S.lane == 0) ? (uint32_t)S.T->ovi[dst] : obs_links;   // m_map_overlay_array[dst]
+        // obs[0] = m_map_overlay_array[dst] (the identity on identity overlays)
+        const uint32_t o = (S.lane == 0) ? (tun ? (uint32_t)S.T->ovi[dst] : dst) : obs_links;
         CNT_ADD(S, decisions, 1u);
         // --train: the answer to this notification also echoes a small-signalling
         // packet to the last hop, unless this node is the packet's source (:303-306)
@@ -1080,7 +1081,7 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
             uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
             double U = (double)u53 * (1.0 / 9007199254740992.0);
             t = sec_to_ns(0.0001 + U);                              // sim.cc:610-630
-            s = (uint32_t)L.N() + f;
+            s = (uint32_t)L.NO() + f;                          // after the NO ping timers
         }
         R.fk_lo.v[j] = lo32(t); R.fk_hi.v[j] = hi32(t); R.fk_seq.v[j] = s; R.f_draw.v[j] = 0;
     }
@@ -1097,7 +1098,7 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
     H.now = 0;
     H.ping_t = L.ping_period();                                       // data-packet-manager.cc:118-121
     H.ping_seq = 0;
-    H.seq = (uint32_t)L.N() + (uint32_t)L.F();
+    H.seq = (uint32_t)L.NO() + (uint32_t)L.F();
     H.uid = 0; H.ping_rounds = 0; H.pend = 0; H.over = 0; H.error = 0; H.stop = 0;
     H.dec = dec; H.hops_launch = hl; H.ev_launch = el;
     H.episode = episode;
