@@ -226,7 +226,7 @@ def main():
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": eng.kernel_name, "kernel_ms": kern_ms, "kernel_source": kernel_source_hash(),
+                "kernel": eng.kernel_name_mlp if args.policy == "dqn_buffer" else eng.kernel_name, "kernel_ms": kern_ms, "kernel_source": kernel_source_hash(),
                 "alg_bytes_per_launch": alg_bytes, "hops_per_launch": hops_per_launch,
             },
             "errors": errors,

@@ -274,6 +274,8 @@ struct Sim {
     unsigned char* logrep;
     uint32_t gid;
     int lane;
+    bool tun;                               // tunnelled overlay: a compile-time constant in the
+                                            // step kernels (template TUN), folded after inlining
 #if PRISMA_TIMING
     mutable uint64_t tsub[2], tlast;             // sub-phase cycles inside apply_decision
 #endif
@@ -298,6 +300,7 @@ __device__ inline void sim_bind(Sim& S, const LV& L, unsigned char* lds, const u
     S.logrep = logrep;
     S.gid = gid;
     S.lane = lane;
+    S.tun = L.tunnels() != 0u;
 }
 
 // uniform LDS reads (every lane reads the same address: broadcast, no conflict)
@@ -508,7 +511,7 @@ __device__ __forceinline__ uint32_t observe_links(const Sim& S, const Regs<FS, L
     const int lane = S.lane;
     uint32_t src = (uint32_t)(r0 + lane - 1);
     const bool pobs = S.lv.ping_as_obs() != 0u;
-    if (!pobs && S.lv.tunnels()) {
+    if (!pobs && S.tun) {
         const bool act = lane >= 1 && lane <= deg;
         src = act ? ti_link(S.T->tinfo[act ? src : 0u]) : 0u;
     }
@@ -611,7 +614,7 @@ __device__ __forceinline__ uint32_t route(const Sim& S, uint32_t x, uint32_t y) 
 }
 // first link of tunnel t
 __device__ __forceinline__ uint32_t tunnel_link(const Sim& S, uint32_t t) {
-    return S.lv.tunnels() ? ti_link(S.T->tinfo[t]) : t;
+    return S.tun ? ti_link(S.T->tinfo[t]) : t;
 }
 
 // DataPacketManager::sendPacket (data-packet-manager.cc:251-299) for decision
@@ -692,7 +695,7 @@ __device__ __forceinline__ void on_ping_round(const Sim& S, Regs<FS, LS>& R, Hot
     uint32_t k = H.ping_rounds;
     uint32_t first_rearm = 0;
     for (int i = 0; i < L.NO(); ++i) {                            // timers in overlay order (sim.cc:528-546)
-        const int u = S.T->ovnode[i];
+        const int u = S.tun ? S.T->ovnode[i] : i;
         const int r0 = S.T->ovrow[u], r1 = S.T->ovrow[u + 1];
         for (int t = r0; t < r1; ++t) {
             if (!link_send(S, R, H, tunnel_link(S, (uint32_t)t), p_make(T_PFWD, (uint32_t)t, 0u, k)))
@@ -908,7 +911,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     const uint32_t x = u_ld32(&S.ring[ring_off(L, l) + k.head]);
     const uint32_t type = ent_type(x);
     const uint32_t v = (uint32_t)S.T->ldst[l];
-    const bool tun = L.tunnels() != 0u;
+    const bool tun = S.tun;
     if (ent_is_data(x)) {
         // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
         // A forwarded packet's previous decision record (t_ns, uid, dst,
@@ -1034,21 +1037,25 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             // responder position on the tunnel: its own delay slot
             const uint32_t pos = tun ? (route(S, ti_org(ti), v) >> 8) - 1u : 0u;
             const float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
-            if (S.lane == 0) S.pbd[(t * L.PLEN() + pos) * L.PBK() + (rnd & (L.PBK() - 1))] = delay;
+            const uint32_t slot = tun ? (t * L.PLEN() + pos) : t;
+            if (S.lane == 0) S.pbd[slot * L.PBK() + (rnd & (L.PBK() - 1))] = delay;
             if (!link_send(S, R, H, (uint32_t)S.T->lrev[l], p_make(T_PBACK, t, pos, rnd))) CNT_ADD(S, ctrl_dropped, 1u);
         }
         if (tgt != v) { ctrl_forward(S, R, H, v, tgt, x); return 0; }
     } else {                                                        // ping-back-packet-manager.cc:120-144
         const uint32_t org = tun ? ti_org(ti) : v;
         if (ovl) {
-            const uint32_t pos = p_pos(x);
-            const float delay = __uint_as_float(
-                u_ld32((const uint32_t*)S.pbd + (t * L.PLEN() + pos) * L.PBK() + (rnd & (L.PBK() - 1))));
-            // the ORIGIN's tunnel index applied to this node's own tunnel list
-            const uint32_t idx = t - (uint32_t)S.T->ovrow[org];
-            const uint32_t v0 = (uint32_t)S.T->ovrow[v];
-            if (idx >= (uint32_t)S.T->ovrow[v + 1] - v0) fail(H, PRISMA_EBIT_PINGIDX);
-            else ping_ack(S, R, H, v0 + idx, rnd, delay);
+            const uint32_t slot = tun ? (t * L.PLEN() + p_pos(x)) : t;
+            const float delay = __uint_as_float(u_ld32((const uint32_t*)S.pbd + slot * L.PBK() + (rnd & (L.PBK() - 1))));
+            if (!tun) {
+                ping_ack(S, R, H, t, rnd, delay);                  // identity: tunnel == link
+            } else {
+                // the ORIGIN's tunnel index applied to this node's own tunnel list
+                const uint32_t idx = t - (uint32_t)S.T->ovrow[org];
+                const uint32_t v0 = (uint32_t)S.T->ovrow[v];
+                if (idx >= (uint32_t)S.T->ovrow[v + 1] - v0) fail(H, PRISMA_EBIT_PINGIDX);
+                else ping_ack(S, R, H, v0 + idx, rnd, delay);
+            }
         }
         if (org != v) { ctrl_forward(S, R, H, v, org, x); return 0; }
     }
@@ -1313,7 +1320,7 @@ template <int FS, int LS> struct StepOcc {
 
 // MLP: the in-kernel DQN-buffer policy is compiled in (mode 4 only); the table /
 // external instances carry none of its code or registers.
-template <int FS, int LS, bool MLP>
+template <int FS, int LS, bool MLP, bool TUN>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(StepOcc<FS, LS>::waves)))
 prisma_step_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -1326,6 +1333,7 @@ prisma_step_kernel_t(KParams P) {
     __syncthreads();
     Sim S;
     sim_bind(S, lv, lds, P.topo, P.log + (size_t)r * LC.log_cap * LC.rec_bytes, LC.replica_base + (uint32_t)r, lane);
+    S.tun = TUN;
     const LV& L = S.lv;
     const bool mlp_mode = MLP;
     const bool table_mode = (P.mode == 2) || mlp_mode;            // fused in-kernel policy
@@ -1443,15 +1451,22 @@ prisma_step_kernel_t(KParams P) {
 // instantiations: flow slots FS in {1,2,4,8} (F <= 512), link slots LS in {1,2,4} (L <= 256)
 typedef void (*kernel_fn)(KParams);
 template <int FS, int LS> struct KPair {
-    static const void* step() { return (const void*)prisma_step_kernel_t<FS, LS, false>; }
-    static const void* step_mlp() { return (const void*)prisma_step_kernel_t<FS, LS, true>; }
+    static const void* step(bool tun) {
+        return tun ? (const void*)prisma_step_kernel_t<FS, LS, false, true>
+                   : (const void*)prisma_step_kernel_t<FS, LS, false, false>;
+    }
+    static const void* step_mlp(bool tun) {
+        return tun ? (const void*)prisma_step_kernel_t<FS, LS, true, true>
+                   : (const void*)prisma_step_kernel_t<FS, LS, true, false>;
+    }
     static const void* reset() { return (const void*)prisma_reset_kernel_t<FS, LS>; }
 };
 
-// which: 0 step (table / external), 1 reset, 2 step with the DQN-buffer policy
-static const void* pick_kernel(int fs, int ls, int which) {
+// which: 0 step (table / external), 1 reset, 2 step with the DQN-buffer policy;
+// tun: tunnelled-overlay instance (identity overlays run code without the tunnel paths)
+static const void* pick_kernel(int fs, int ls, int which, bool tun) {
 #define PK(F_, L_) if (fs == F_ && ls == L_) \
-    return which == 1 ? KPair<F_, L_>::reset() : (which == 2 ? KPair<F_, L_>::step_mlp() : KPair<F_, L_>::step());
+    return which == 1 ? KPair<F_, L_>::reset() : (which == 2 ? KPair<F_, L_>::step_mlp(tun) : KPair<F_, L_>::step(tun));
     PK(1, 1) PK(1, 2) PK(1, 4) PK(2, 1) PK(2, 2) PK(2, 4) PK(4, 1) PK(4, 2) PK(4, 4) PK(8, 1) PK(8, 2) PK(8, 4)
 #undef PK
     return nullptr;
@@ -1841,9 +1856,9 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
         prisma_destroy(e);
         return set_err(PRISMA_ERR_DEVICE, "device initialisation failed");
     }
-    e->k_step = pick_kernel(L.FS, L.LS, 0);
-    e->k_reset = pick_kernel(L.FS, L.LS, 1);
-    e->k_step_mlp = pick_kernel(L.FS, L.LS, 2);
+    e->k_step = pick_kernel(L.FS, L.LS, 0, L.tunnels != 0u);
+    e->k_reset = pick_kernel(L.FS, L.LS, 1, false);
+    e->k_step_mlp = pick_kernel(L.FS, L.LS, 2, L.tunnels != 0u);
     (void)hipFuncSetAttribute(e->k_step_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes + 256);
     (void)hipFuncSetAttribute(e->k_step, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
     (void)hipFuncSetAttribute(e->k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);

@@ -187,9 +187,12 @@ class PrismaEngine:
         fs, ls = 1, 1
         while 64 * fs < topo.n_flows:
             fs *= 2
-        while 64 * ls < topo.n_links + topo.n_nodes:
+        while 64 * ls < max(topo.n_links + topo.n_nodes, topo.n_tunnels):
             ls *= 2
-        self.kernel_name = f"prisma_step_kernel_t<{fs}, {ls}>"
+        tun = "false" if topo.identity else "true"
+        # step-kernel instance (demangled name prefix; the third argument is the in-kernel MLP)
+        self.kernel_name = f"prisma_step_kernel_t<{fs}, {ls}, false, {tun}>"
+        self.kernel_name_mlp = f"prisma_step_kernel_t<{fs}, {ls}, true, {tun}>"
         self.obs = torch.zeros((self.R, self.W), dtype=torch.int32, device=self.torch_device)
         self.mask = torch.zeros(self.R, dtype=torch.uint8, device=self.torch_device)
         self.node = torch.zeros(self.R, dtype=torch.int32, device=self.torch_device)
