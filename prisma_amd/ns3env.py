@@ -120,6 +120,7 @@ class PrismaSession:
         self.engine = PrismaEngine(self.topo, self.params, 1, device)
         self.base_port = int(base_port)
         self.N = self.topo.n_nodes
+        self.n_agents = self.topo.n_overlay                               # ports base .. base + NO - 1
         self.deg = [int(d) for d in self.topo.degrees]
         self.data_size = int(self.params["packet_size"]) + 30          # UDP 8 + IP 20 + PPP 2
         self._cv = threading.Condition()
@@ -186,7 +187,7 @@ class PrismaSession:
     def close(self):
         with self._cv:
             self._closed += 1
-            if self._closed >= self.N or self._over:
+            if self._closed >= self.n_agents or self._over:
                 self._over = True
                 self._cv.notify_all()
 
@@ -207,7 +208,7 @@ class PrismaSession:
 
 def session_for_port(port: int) -> PrismaSession:
     for s in reversed(_SESSIONS):
-        if s.base_port <= port < s.base_port + s.N:
+        if s.base_port <= port < s.base_port + s.n_agents:
             return s
     raise RuntimeError(f"no PrismaSession serves port {port}: create one with PrismaSession(base_port=...)")
 
@@ -224,7 +225,8 @@ class _BridgeShim:
 
 
 class Ns3Env:
-    """ns3env.Ns3Env signature; node = port - session.base_port.
+    """ns3env.Ns3Env signature; overlay index = port - session.base_port (the env of overlay
+    node i listens on openGymPort + i, sim.cc:528-535); `node` is its underlay id.
 
     Like the reference, the constructor returns at once with the start-up
     state every node's PacketRoutingEnv::initialize() notifies (sim.cc:546,
@@ -237,7 +239,7 @@ class Ns3Env:
         self.stepTime, self.port, self.startSim = stepTime, port, startSim
         self.simSeed, self.simArgs, self.debug = simSeed, simArgs, debug
         self.session = session if session is not None else session_for_port(int(port))
-        self.node = int(port) - self.session.base_port
+        self.node = int(self.session.topo.overlay_nodes[int(port) - self.session.base_port])
         deg = self.session.deg[self.node]
         self.action_space = Discrete(deg)
         self.observation_space = Box(0, 16260, (1 + deg,))

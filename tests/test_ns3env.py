@@ -39,8 +39,11 @@ def oracle_stream(oracle_mod, topo, params, policy, n):
 
 
 def sp_policy(topo):
+    """forwarder.py:149,190-191: action 0 at the destination (obs[0] == own overlay index)
+    and for control notifications, else the SP next hop on the overlay graph."""
     table = sp_next_hop_table(topo)
-    return lambda v, obs: 0 if obs[0] in (v, 1000) else int(table[v, obs[0]])
+    on, ovi = topo.overlay_nodes, topo.overlay_index
+    return lambda v, obs: 0 if obs[0] in (ovi[v], 1000) else int(table[v, on[obs[0]]])
 
 
 def test_info_renderer_matches_oracle(oracle_mod):
@@ -97,10 +100,11 @@ def test_notify_dest_does_not_change_the_trajectory(oracle_mod):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")
-@pytest.mark.parametrize("train", [0, 1])
-def test_session_stream_matches_oracle(oracle_mod, train):
+@pytest.mark.parametrize("name,lf,train", [("abilene", 2.0, 0), ("abilene", 2.0, 1),
+                                           ("overlay_full_mesh_3n_abilene", 10.0, 1)])
+def test_session_stream_matches_oracle(oracle_mod, name, lf, train):
     from prisma_amd.ns3env import PrismaSession
-    topo = Topology.example("abilene", 0, 2.0)
+    topo = Topology.example(name, 0, lf)
     kw = dict(sim_time_s=2.0, ping_as_obs=1, train=train)
     pol = sp_policy(topo)
     _, ref = oracle_stream(oracle_mod, topo, engine_params(topo, notify_dest=1, **kw), pol, 1500)
@@ -117,22 +121,25 @@ def test_session_stream_matches_oracle(oracle_mod, train):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")
-def test_threaded_per_node_envs(oracle_mod):
-    """One Forwarder-like thread per node over Ns3Env(port=base+node)."""
+@pytest.mark.parametrize("name,lf", [("abilene", 1.0), ("overlay_full_mesh_3n_abilene", 10.0)])
+def test_threaded_per_node_envs(oracle_mod, name, lf):
+    """One Forwarder-like thread per overlay node over Ns3Env(port=base+index)."""
     from prisma_amd.ns3env import Ns3Env, PrismaSession
-    topo = Topology.example("abilene")
+    topo = Topology.example(name, 0, lf)
     kw = dict(sim_time_s=1.5, ping_as_obs=1)
     pol = sp_policy(topo)
     s = PrismaSession(topo=topo, base_port=7100, **kw)
-    seen = {u: [] for u in range(topo.n_nodes)}
+    nodes = [int(x) for x in topo.overlay_nodes]
+    seen = {u: [] for u in nodes}
     errors = []
 
     # the reference builds every node's env in the main thread first (main.py:118-127)
-    envs = [Ns3Env(port=7100 + u, stepTime=0, startSim=0, simSeed=100) for u in range(topo.n_nodes)]
+    envs = {u: Ns3Env(port=7100 + i, stepTime=0, startSim=0, simSeed=100) for i, u in enumerate(nodes)}
 
     def forwarder(u):
         try:
             env = envs[u]
+            assert env.node == u
             obs = env.reset()
             assert obs == [-1]
             obs, _, done, info = env.step(0)        # start-up state: the answer is ignored
@@ -143,14 +150,14 @@ def test_threaded_per_node_envs(oracle_mod):
         except Exception as e:                       # pragma: no cover - surfaced below
             errors.append(e)
 
-    ths = [threading.Thread(target=forwarder, args=(u,)) for u in range(topo.n_nodes)]
+    ths = [threading.Thread(target=forwarder, args=(u,)) for u in nodes]
     for t in ths:
         t.start()
     for t in ths:
         t.join(timeout=600)
     assert not errors and not any(t.is_alive() for t in ths)
     o, ref = oracle_stream(oracle_mod, topo, engine_params(topo, notify_dest=1, **kw), pol, 10 ** 9)
-    for u in range(topo.n_nodes):
+    for u in nodes:
         assert seen[u] == [obs for (v, obs, _, _) in ref if v == u], u
     got, want = s.counters(), o.counters()
     for k in ("hops", "decisions", "ov_injected", "ov_arrived", "ov_lost", "reward_sum", "cost_sum", "dec_count"):
