@@ -36,7 +36,7 @@ import numpy as np
 from .config import engine_params
 from .engine import PrismaEngine
 from .env import Box, Discrete
-from .records import ST_DESTINATION, ST_DROPPED, ST_PENDING
+from .records import ST_DESTINATION, ST_DROPPED, ST_ENQUEUED, ST_PENDING
 from .topology import Topology
 
 _SESSIONS: List["PrismaSession"] = []
@@ -129,6 +129,7 @@ class PrismaSession:
         self._pending = None                                             # (node, obs, done, info, dec)
         self._over = False
         self._closed = 0
+        self._inflight: Dict[int, int] = {}                              # tunnel hops not yet arrived: dec -> uid
         self.log: List[tuple] = []                                       # (node, obs, done, info) per notify
         self.engine.reset(0)
         self._advance(None)
@@ -142,7 +143,12 @@ class PrismaSession:
         obs, mask, node = self.engine.step(a)
         cnt = self.engine.counters()[0]
         if prev is not None and prev[4] is not None:
-            self.tracker.applied(self.engine.records(0, prev[4], 1)[0])
+            rec = self.engine.records(0, prev[4], 1)[0]
+            self.tracker.applied(rec)
+            if not self.topo.identity and int(rec["status"]) == ST_ENQUEUED:
+                self._inflight[prev[4]] = int(rec["uid"])
+        if self._inflight:
+            self._poll_tunnel_drops(int(cnt["dec_count"]))
         if int(mask.cpu()[0]) == 0:
             self._pending = None
             self._over = True
@@ -158,11 +164,34 @@ class PrismaSession:
             rec = self.engine.records(0, d, 1)[0]
             assert int(rec["status"]) in (ST_PENDING, ST_DESTINATION)
             ob = [int(x) for x in row[:1 + self.deg[v]]]
+            self._inflight.pop(int(rec["prev"]), None)                   # the hop arrived
             self.tracker.notified(rec)
             done = int(rec["status"]) == ST_DESTINATION
             self._last_done[v] = done
             self._pending = (v, ob, done, self.tracker.render(rec, cnt), d)
         self.log.append(self._pending[:4])
+
+    def _poll_tunnel_drops(self, dec_count: int):
+        """Tunnelled overlays: a packet can be dropped on an intermediate FIFO after its
+        decision was applied; the engine then re-marks that record DROPPED (MacTxDrop ->
+        the sender's dropPacket, data-packet-manager.cc:88-106).  Polled after every engine
+        step, i.e. at the same point of the event stream as the reference; several such
+        drops inside one step are listed in decision order (the reference: drop order)."""
+        import torch
+        cap = self.engine.log_capacity
+        for d in [d for d in self._inflight if d < dec_count - cap // 2]:
+            del self._inflight[d]                                         # TTL-expired, never arrives
+        if not self._inflight:
+            return
+        ds = sorted(self._inflight)
+        dev = self.engine.torch_device
+        raw = self.engine.gather_records(torch.zeros(len(ds), dtype=torch.int32, device=dev),
+                                         torch.tensor(ds, dtype=torch.int32, device=dev)).cpu().numpy()
+        recs = raw.reshape(-1).view(self.engine.rec_dtype)
+        for d, rec in zip(ds, recs):
+            if int(rec["status"]) == ST_DROPPED:
+                self.tracker.applied(rec)
+                del self._inflight[d]
 
     # -- single-threaded driver (tests, notebooks) -----------------------------
     def pending(self):
