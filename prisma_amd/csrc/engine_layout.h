@@ -105,6 +105,9 @@ struct TopoImage {
     uint32_t tinfo[256];         // tunnel t: first link | target << 8 | origin << 16 | links << 24
     int32_t ovi[256];            // overlay index of node x (obs[0] of a packet for x), -1 if none
     int32_t ovnode[256];         // underlay id of overlay node i (ping timers, overlay order)
+    uint32_t rinfo[256];         // tunnelled overlays: ring of link l = entries [off, off + cap): off | cap << 16
+    uint32_t tresp[256];         // tunnelled overlays: ping-back delay slot base of tunnel t | responder
+                                 // position mask << 16 (overlay nodes on the tunnel, target included)
     // uint32_t route[N][N] follows (tunnelled overlays only): next link x -> y | hops(x, y) << 8
 };
 __host__ __device__ inline uint32_t ti_link(uint32_t ti) { return ti & 255u; }
@@ -122,6 +125,7 @@ struct Layout {
     int32_t  T, NO;              // tunnels, overlay nodes
     uint32_t tunnels;            // 1: tunnelled overlay (route table present)
     uint32_t PLEN;               // responder positions per tunnel (max tunnel length)
+    uint32_t ring_total;         // packet slots over all link FIFOs
     uint32_t lds_state_bytes;    // LDS part of the image (bytes [0, lds_state_bytes))
     uint32_t s_regs;             // register part: 4 x [64*FS] + 19 x [64*LS] u32 arrays
     uint32_t PBK;                // ping-back delay slots per (tunnel, position) (power of two)

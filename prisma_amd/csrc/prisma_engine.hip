@@ -224,6 +224,7 @@ struct LV {
     __device__ __forceinline__ int32_t NO() const { return (int32_t)u(offsetof(Layout, NO) / 4); }
     __device__ __forceinline__ uint32_t tunnels() const { return (uint32_t)u(offsetof(Layout, tunnels) / 4); }
     __device__ __forceinline__ uint32_t PLEN() const { return (uint32_t)u(offsetof(Layout, PLEN) / 4); }
+    __device__ __forceinline__ uint32_t ring_total() const { return (uint32_t)u(offsetof(Layout, ring_total) / 4); }
     __device__ __forceinline__ uint32_t lds_state_bytes() const { return (uint32_t)u(offsetof(Layout, lds_state_bytes) / 4); }
     __device__ __forceinline__ uint32_t s_regs() const { return (uint32_t)u(offsetof(Layout, s_regs) / 4); }
     __device__ __forceinline__ uint32_t PBK() const { return (uint32_t)u(offsetof(Layout, PBK) / 4); }
@@ -266,7 +267,7 @@ struct Sim {
     uint32_t* wt; uint32_t* wseq;           // wire: arrival time (low 32 bits) and seq
     uint32_t* ring;
     float* win;
-    float* pbd;                             // ping-back delays [T][PLEN][PBK]
+    float* pbd;                             // ping-back delays [responder slot][PBK]
     const CAS TopoImage* T;                 // topology (scalar loads at fixed offsets)
     const uint8_t* table;
     const float* mlp;                       // DQN-buffer weights (HBM) or null
@@ -354,10 +355,18 @@ __device__ __forceinline__ bool key_less(int64_t t, uint32_t s, int64_t bt, uint
 __device__ __forceinline__ uint32_t ent_size(const LV& L, uint32_t x) {
     return ent_is_data(x) ? L.data_size() : (ent_is_echo(x) ? L.echo_size() : L.ping_size());
 }
-__device__ __forceinline__ uint32_t ring_off(const LV& L, uint32_t l) {
+// FIFO ring of link l: uniform capacities on identity overlays, per-link (sized by the
+// control traffic crossing each link) on tunnelled ones
+__device__ __forceinline__ uint32_t ring_off(const Sim& S, uint32_t l) {
+    const LV& L = S.lv;
+    if (S.tun) return S.T->rinfo[l] & 0xffffu;
     return l < (uint32_t)L.E() ? l * L.qcap_s() : (uint32_t)L.E() * L.qcap_s() + (l - (uint32_t)L.E()) * L.qcap_a();
 }
-__device__ __forceinline__ uint32_t ring_cap(const LV& L, uint32_t l) { return l < (uint32_t)L.E() ? L.qcap_s() : L.qcap_a(); }
+__device__ __forceinline__ uint32_t ring_cap(const Sim& S, uint32_t l) {
+    const LV& L = S.lv;
+    if (S.tun) return S.T->rinfo[l] >> 16;
+    return l < (uint32_t)L.E() ? L.qcap_s() : L.qcap_a();
+}
 
 // one link's fields as uniform scalars
 struct LinkV {
@@ -432,7 +441,7 @@ __device__ __forceinline__ int link_send(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     uint32_t size = ent_size(L, e);
     bool ok = l < (uint32_t)L.E() ? (k.qb + size <= L.qmax_bytes()) : (k.n_queue + 1u <= L.acc_qmax_pkts());
     if (!ok) return 0;
-    uint32_t cap = ring_cap(L, l), off = ring_off(L, l);
+    uint32_t cap = ring_cap(S, l), off = ring_off(S, l);
     if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
     if (S.lane == 0) S.ring[off + k.tail] = e;
     k.tail = (k.tail + 1 == cap) ? 0 : k.tail + 1;
@@ -457,9 +466,9 @@ __device__ __forceinline__ void on_complete(const Sim& S, Regs<FS, LS>& R, Hot& 
     LinkV k = link_get(R, l);
     k.busy = 0;
     if (k.n_queue) {
-        uint32_t cap = ring_cap(L, l);
+        uint32_t cap = ring_cap(S, l);
         uint32_t xi = k.txp;
-        uint32_t hx = u_ld32(&S.ring[ring_off(L, l) + xi]);
+        uint32_t hx = u_ld32(&S.ring[ring_off(S, l) + xi]);
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
@@ -819,7 +828,7 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
 template <int FS, int LS>
 __device__ __forceinline__ void wire_pop(const Sim& S, Regs<FS, LS>& R, const Hot& H, uint32_t l, LinkV& k) {
     const LV& L = S.lv;
-    const uint32_t cap = ring_cap(L, l);
+    const uint32_t cap = ring_cap(S, l);
     k.head = (k.head + 1 == cap) ? 0 : k.head + 1;
     k.n_wire--;
     if (k.n_wire) {                                                 // next packet on the wire
@@ -903,12 +912,19 @@ __device__ __forceinline__ void ping_ack(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     R.pav_hi.set(lt, (uint32_t)(avg >> 32));
 }
 
+// ping-back delay slot of responder position pos on tunnel t (tunnelled overlays): one
+// slot per overlay node on the tunnel
+__device__ __forceinline__ uint32_t pbd_slot(const Sim& S, uint32_t t, uint32_t pos) {
+    const uint32_t tr = S.T->tresp[t];
+    return (tr & 0xffffu) + (uint32_t)__builtin_popcount((tr >> 16) & ((1u << pos) - 1u));
+}
+
 // returns 1 if a data decision needs an action
 template <int FS, int LS>
 __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t l, Decision& D, bool fused) {
     const LV& L = S.lv;
     LinkV k = link_get(R, l);
-    const uint32_t x = u_ld32(&S.ring[ring_off(L, l) + k.head]);
+    const uint32_t x = u_ld32(&S.ring[ring_off(S, l) + k.head]);
     const uint32_t type = ent_type(x);
     const uint32_t v = (uint32_t)S.T->ldst[l];
     const bool tun = S.tun;
@@ -1037,7 +1053,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
             // responder position on the tunnel: its own delay slot
             const uint32_t pos = tun ? (route(S, ti_org(ti), v) >> 8) - 1u : 0u;
             const float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
-            const uint32_t slot = tun ? (t * L.PLEN() + pos) : t;
+            const uint32_t slot = tun ? pbd_slot(S, t, pos) : t;
             if (S.lane == 0) S.pbd[slot * L.PBK() + (rnd & (L.PBK() - 1))] = delay;
             if (!link_send(S, R, H, (uint32_t)S.T->lrev[l], p_make(T_PBACK, t, pos, rnd))) CNT_ADD(S, ctrl_dropped, 1u);
         }
@@ -1045,7 +1061,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, Regs<FS, LS>& R, Hot& H, 
     } else {                                                        // ping-back-packet-manager.cc:120-144
         const uint32_t org = tun ? ti_org(ti) : v;
         if (ovl) {
-            const uint32_t slot = tun ? (t * L.PLEN() + p_pos(x)) : t;
+            const uint32_t slot = tun ? pbd_slot(S, t, p_pos(x)) : t;
             const float delay = __uint_as_float(u_ld32((const uint32_t*)S.pbd + slot * L.PBK() + (rnd & (L.PBK() - 1))));
             if (!tun) {
                 ping_ack(S, R, H, t, rnd, delay);                  // identity: tunnel == link
@@ -1530,9 +1546,14 @@ static uint32_t next_pow2(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; r
 // Overlay of a topology (host): tunnels, routing, control-packet load per link.
 struct OverlayPlan {
     bool tunnels = false;                // false: identity overlay (tunnel t == link t)
-    int T = 0, NO = 0, maxdeg = 0, plen = 1, ctrl_max = 2, echo_max = 1;
+    int T = 0, NO = 0, maxdeg = 0, plen = 1;
     std::vector<int32_t> ovrow, ovi, ovnode;
     std::vector<uint32_t> tinfo, route;  // route: [N][N] next link | hops << 8
+    std::vector<uint32_t> tresp;         // pbd slot base | responder position mask << 16
+    int n_resp = 0;                      // ping responders over all tunnels (pbd slots)
+    // control-packet routes (links in order), each starting when its ping round
+    // (or, for echoes, the data arrival) fires: pings, ping-backs, echoes
+    std::vector<std::vector<int>> cpaths, epaths;
 };
 
 // ns-3 global routing restated for unit link metrics: the SPF
@@ -1609,9 +1630,9 @@ static int plan_overlay(const prisma_topology_t* T, OverlayPlan& OP) {
     for (int i = 0; i < NO && ident; ++i) ident = (OP.ovnode[i] == i);
     OP.tunnels = !ident;
     OP.tinfo.resize(OP.T);
-    std::vector<int> c_ping(E, 0), c_echo(E, 0);
-    auto walk = [&](int x, int y, std::vector<int>& cnt) {   // count links of the route x -> y
-        while (x != y) { const int l = hop[(size_t)x * N + y]; cnt[l]++; x = T->link_dst[l]; }
+    OP.tresp.resize(OP.T);
+    auto route_links = [&](int x, int y, std::vector<int>& out) {   // append the route x -> y
+        while (x != y) { const int l = hop[(size_t)x * N + y]; out.push_back(l); x = T->link_dst[l]; }
     };
     for (int t = 0; t < OP.T; ++t) {
         const int u = tsrc[t], w = tdst[t];
@@ -1623,22 +1644,29 @@ static int plan_overlay(const prisma_topology_t* T, OverlayPlan& OP) {
         // forward path of the pings; a ping-back from every overlay node on it
         // (reverse of the arrival link, then routed to the origin); the --train
         // echo from the target likewise
-        walk(u, w, c_ping);
+        std::vector<int> fwd;
+        route_links(u, w, fwd);
+        OP.cpaths.push_back(fwd);
+        uint32_t mask = 0;
         int x = u;
-        while (x != w) {
-            const int l = hop[(size_t)x * N + w], nxt = T->link_dst[l];
+        for (int i = 0; i < len; ++i) {
+            const int l = fwd[i], nxt = T->link_dst[l];
             if (OP.ovi[nxt] >= 0) {
-                c_ping[T->link_rev[l]]++;
-                walk(x, u, c_ping);
-                if (nxt == w) { c_echo[T->link_rev[l]]++; walk(x, u, c_echo); }
+                mask |= 1u << i;
+                std::vector<int> rp(fwd.begin(), fwd.begin() + i + 1);
+                rp.push_back(T->link_rev[l]);
+                route_links(x, u, rp);
+                OP.cpaths.push_back(rp);
+                if (nxt == w) {
+                    std::vector<int> ep(1, T->link_rev[l]);
+                    route_links(x, u, ep);
+                    OP.epaths.push_back(ep);
+                }
             }
             x = nxt;
         }
-    }
-    OP.ctrl_max = 2; OP.echo_max = 1;
-    for (int l = 0; l < E; ++l) {
-        OP.ctrl_max = c_ping[l] > OP.ctrl_max ? c_ping[l] : OP.ctrl_max;
-        OP.echo_max = c_echo[l] > OP.echo_max ? c_echo[l] : OP.echo_max;
+        OP.tresp[t] = (uint32_t)OP.n_resp | (mask << 16);
+        OP.n_resp += __builtin_popcount(mask);
     }
     if (OP.tunnels) {
         OP.route.assign((size_t)N * N, 0u);
@@ -1729,26 +1757,56 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.WCAP = (int)next_pow2(wire < 2 ? 2 : wire);
     if (L.WCAP > 64) return set_err(PRISMA_ERR_CONFIG, "propagation delay too long for the wire model");
     // ring capacity: full byte-limited FIFO of data + the control packets that
-    // can be queued at once: per round, the pings and ping-backs whose route
-    // crosses the link (2 on identity overlays), over the time a ping can spend
-    // on its round trip (2 * tunnel length FIFOs and wires)
+    // can be queued at once + the packets on the wire.
     double drain_s = (double)P->max_buffer_bytes * 8.0 / (double)P->link_bps + (double)L.sw_txd * 1e-9;
-    double span = 2.0 * (double)OP.plen * (drain_s + (double)P->link_delay_ns * 1e-9);
-    uint32_t ctrl = (uint32_t)OP.ctrl_max * ((uint32_t)(span / (double)P->ping_interval_s) + 3u);
-    // --train echoes on a link answer data packets that crossed a tunnel whose
-    // echo route uses the link; per tunnel they arrive at least one data
-    // transmission apart: at most drain/tx_data + 2 of them wait in a FIFO at once
-    uint32_t echoes = L.train ? (uint32_t)OP.echo_max * ((uint32_t)(drain_s / ((double)L.sw_txd * 1e-9)) + 2u) : 0u;
-    uint32_t qs = P->max_buffer_bytes / L.data_size + ctrl + echoes + (uint32_t)L.WCAP;
-    qs = (qs + (uint32_t)L.WCAP - 1) / (uint32_t)L.WCAP * (uint32_t)L.WCAP;
-    if (qs > 65535u) return set_err(PRISMA_ERR_CONFIG, "queue too deep");
-    L.qcap_s = qs;
+    const double tx_s = (double)L.sw_txd * 1e-9, ival = (double)P->ping_interval_s;
+    const uint32_t data_max = P->max_buffer_bytes / L.data_size;
+    std::vector<uint32_t> rcap(E);
+    double span;
+    if (!OP.tunnels) {
+        // identity: per round one ping and one ping-back cross a link, each within
+        // two FIFOs and wires of its round; echoes answer data packets that crossed
+        // the reverse link, at least one data transmission apart
+        span = 2.0 * (drain_s + (double)P->link_delay_ns * 1e-9);
+        const uint32_t ctrl = 2u * ((uint32_t)(span / ival) + 3u);
+        const uint32_t echoes = L.train ? (uint32_t)(drain_s / tx_s) + 2u : 0u;
+        uint32_t qs = data_max + ctrl + echoes + (uint32_t)L.WCAP;
+        qs = (qs + (uint32_t)L.WCAP - 1) / (uint32_t)L.WCAP * (uint32_t)L.WCAP;
+        for (int l = 0; l < E; ++l) rcap[l] = qs;
+    } else {
+        // tunnelled: per link, every control route through it contributes the
+        // rounds (echoes: data arrivals, >= one transmission apart) whose packets
+        // can still sit in its FIFO: a packet at the d-th FIFO of its route left
+        // its round's start at most d * (drain + 2 tx + propagation) before
+        const double hop_s = (double)P->max_buffer_bytes * 8.0 / (double)P->link_bps + 2.0 * tx_s +
+                             (double)P->link_delay_ns * 1e-9;
+        std::vector<double> c(E, 0.0);
+        for (const auto& pth : OP.cpaths)
+            for (size_t i = 0; i < pth.size(); ++i) c[pth[i]] += (double)((uint32_t)((double)(i + 1) * hop_s / ival) + 1u);
+        if (L.train)
+            for (const auto& pth : OP.epaths)
+                for (size_t i = 0; i < pth.size(); ++i) c[pth[i]] += (double)((uint32_t)((double)(i + 1) * hop_s / tx_s) + 1u);
+        for (int l = 0; l < E; ++l) {
+            uint32_t qs = data_max + (uint32_t)c[l] + (uint32_t)L.WCAP;
+            rcap[l] = (qs + (uint32_t)L.WCAP - 1) / (uint32_t)L.WCAP * (uint32_t)L.WCAP;
+        }
+        span = 2.0 * (double)OP.plen * hop_s;
+    }
+    L.qcap_s = 0;
+    uint32_t tot = 0;
+    for (int l = 0; l < E; ++l) {
+        if (rcap[l] > 65535u) return set_err(PRISMA_ERR_CONFIG, "queue too deep");
+        L.qcap_s = rcap[l] > L.qcap_s ? rcap[l] : L.qcap_s;
+        tot += rcap[l];
+    }
     L.qcap_a = (uint32_t)(L.WCAP < 8 ? 8 : L.WCAP);
-    uint32_t tot = (uint32_t)E * L.qcap_s + (uint32_t)N * L.qcap_a;
-    // ping-back delay slots per (tunnel, responder): round k's slot is reused
-    // by round k + PBK, whose forward ping arrives after round k's ping-back
-    // (at most span after k's send) has been consumed
-    L.PBK = next_pow2((uint32_t)(span / (double)P->ping_interval_s) + 2u);
+    tot += (uint32_t)N * L.qcap_a;
+    if (tot > 65535u) return set_err(PRISMA_ERR_CONFIG, "ring entries exceed the LDS image");
+    L.ring_total = tot;
+    // ping-back delay slots per responder: round k's slot is reused by round
+    // k + PBK, whose forward ping arrives after round k's ping-back (at most
+    // span after k's send) has been consumed
+    L.PBK = next_pow2((uint32_t)(span / ival) + 2u);
     // wire arrival times are kept as their low 32 bits relative to the clock
     int64_t max_acc = 0;
     for (int u = 0; u < N; ++u) max_acc = acctx[u] > max_acc ? acctx[u] : max_acc;
@@ -1775,6 +1833,15 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     memcpy(TI.tinfo, OP.tinfo.data(), 4u * OP.T);
     for (int x = 0; x < N; ++x) TI.ovi[x] = OP.ovi[x];
     memcpy(TI.ovnode, OP.ovnode.data(), 4u * OP.NO);
+    if (OP.tunnels) {
+        uint32_t off = 0;
+        for (int l = 0; l < Lk; ++l) {
+            const uint32_t cap = l < E ? rcap[l] : L.qcap_a;
+            TI.rinfo[l] = off | (cap << 16);
+            off += cap;
+        }
+        memcpy(TI.tresp, OP.tresp.data(), 4u * OP.T);
+    }
     if (OP.tunnels) memcpy(topo.data() + sizeof(TopoImage), OP.route.data(), 4u * (size_t)N * N);
 
     // state image: LDS part (staged into LDS) then register part (staged into VGPRs)
@@ -1795,7 +1862,7 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.s_wseq = take(4u * Lk * L.WCAP);
     L.s_ring = take(4u * tot);
     L.s_win = take(4u * (uint32_t)OP.T * L.MA);
-    L.s_pbd = take(4u * (uint32_t)OP.T * L.PLEN * L.PBK);
+    L.s_pbd = take(4u * (uint32_t)(OP.tunnels ? OP.n_resp : OP.T) * L.PBK);
     L.lds_state_bytes = o;
     L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 19u * 64u * (uint32_t)ls));
     L.state_bytes = o;
@@ -2018,7 +2085,7 @@ extern "C" int prisma_plan(const prisma_topology_t* topo, const prisma_params_t*
     out->state_bytes = L.state_bytes;
     out->lds_bytes = L.lds_bytes;
     out->lds_state_bytes = L.lds_state_bytes;
-    out->ring_entries = (uint32_t)L.E * L.qcap_s + (uint32_t)L.N * L.qcap_a;
+    out->ring_entries = L.ring_total;
     out->record_bytes = L.rec_bytes;
     out->obs_width = L.W;
     out->flow_slots = L.FS;
