@@ -1,0 +1,7 @@
+#!/bin/bash
+# A/B throughput: _ab_old/ (a previous tree, built) vs the working tree, alternating, same box.
+ARGS="$*"
+for i in 1 2; do
+  (cd _ab_old && timeout -k 10 200 python bench.py --cpu-baseline 0 $ARGS | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('old', round(d['value']/1e6,1), round(d['roofline']['kernel_ms'],2))") || exit 1
+  timeout -k 10 200 python bench.py --cpu-baseline 0 $ARGS | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('new', round(d['value']/1e6,1), round(d['roofline']['kernel_ms'],2))" || exit 1
+done

@@ -415,3 +415,19 @@ def test_tunnel_dqn_buffer_parity(oracle_mod):
         assert eng.records(r, 0, len(ref), log_host=log).tobytes() == ref.tobytes(), r
         assert_counters_equal(cnt[r], o.counters(), r)
     eng.close()
+
+
+def test_tunnel_full_size_properties(oracle_mod):
+    """Config 3 size (4096 Abilene-on-GEANT replicas, SP): invariants on every replica,
+    4 random replicas compared record by record."""
+    topo = Topology.example("abilene_on_geant")
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=1)
+    R, H = 4096, 600
+    rng = np.random.default_rng(4)
+    picks = sorted(rng.choice(R, 4, replace=False).tolist())
+    cnt = run_table_both(oracle_mod, topo, params, R, H, sp_next_hop_table(topo), replicas=picks)
+    assert np.all(cnt["error"] == 0)
+    assert np.all(cnt["hops"] == H)
+    assert np.all(cnt["ov_injected"] >= cnt["ov_arrived"] + cnt["ov_lost"])
+    assert np.all(cnt["bytes_data"] == 540 * cnt["ov_injected"])
+    assert len(np.unique(cnt["now_ns"])) > R // 2
