@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PRISMA_ABI_VERSION 5
+#define PRISMA_ABI_VERSION 6
 
 /* status codes */
 #define PRISMA_OK              0
@@ -69,6 +69,14 @@ extern "C" {
                                       N = n_nodes, rows by underlay id; the
                                       one-hot input is obs[0] (the overlay
                                       index of the destination)               */
+
+/* engine selection (prisma_params_t.engine) */
+#define PRISMA_ENGINE_AUTO     0   /* register-resident when the topology fits it */
+#define PRISMA_ENGINE_REGISTER 1   /* replica state in VGPRs + LDS: <= 255 nodes,
+                                      256 links / tunnels, 512 flows             */
+#define PRISMA_ENGINE_MEMORY   2   /* replica state in HBM under an event tree:
+                                      <= 256 nodes, links + flows <= 262 144,
+                                      identity overlays (ER-256)                 */
 
 /* per-decision status (prisma_record_t.status) */
 #define PRISMA_ST_PENDING      0   /* waiting for an action (prisma_step)  */
@@ -150,6 +158,7 @@ typedef struct prisma_params {
                                    non-source node echoes a 30-B small-
                                    signalling packet to its last hop
                                    (data-packet-manager.cc:301-347)        */
+    uint32_t engine;            /* PRISMA_ENGINE_* (0 = auto)              */
 } prisma_params_t;
 
 /*
@@ -304,6 +313,7 @@ typedef struct prisma_plan {
     int32_t  obs_width;
     int32_t  flow_slots;        /* register slots per lane (64 flows each) */
     int32_t  link_slots;        /* register slots per lane (64 links each) */
+    uint32_t engine;            /* PRISMA_ENGINE_REGISTER or _MEMORY       */
 } prisma_plan_t;
 int prisma_plan(const prisma_topology_t* topo, const prisma_params_t* params, prisma_plan_t* out);
 

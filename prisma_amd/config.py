@@ -68,11 +68,14 @@ def engine_params(topo: Topology, *, sim_time_s: float = 60.0, seed: int = 100, 
                   ping_interval_s: float = 0.2, ma_size: int = 5, link_cap: int = 500000,
                   link_delay_ms: float = 1.0, max_buffer: int = 16260, packet_size: int = 512,
                   auto_reset: int = 0, log_capacity: int = 8192, replica_base: int = 0,
-                  loss_penalty: Optional[float] = None, train: int = 0, notify_dest: int = 0) -> dict:
+                  loss_penalty: Optional[float] = None, train: int = 0, notify_dest: int = 0,
+                  engine: int = 0) -> dict:
     """prisma_params_t as a dict (shared by the engine binding and the oracle).
 
     train=1 is the reference's --train: every data notification at a non-source
-    node sends a small-signalling echo back to its last hop."""
+    node sends a small-signalling echo back to its last hop.
+    engine: 0 auto (register-resident when the topology fits it), 1 register-resident,
+    2 memory-resident (include/prisma.h PRISMA_ENGINE_*)."""
     if log_capacity < 1024 or log_capacity > (1 << 22) or log_capacity & (log_capacity - 1):
         raise ValueError("log_capacity must be a power of two in [1024, 2^22]")
     lp = _loss_penalty(max_buffer, packet_size, link_cap, topo.n_overlay) if loss_penalty is None else loss_penalty
@@ -82,5 +85,5 @@ def engine_params(topo: Topology, *, sim_time_s: float = 60.0, seed: int = 100, 
         ping_interval_s=float(ping_interval_s), ma_size=int(ma_size), ping_as_obs=int(ping_as_obs),
         auto_reset=int(auto_reset), loss_penalty=float(lp), seed=int(seed),
         replica_base=int(replica_base), log_capacity=int(log_capacity), notify_dest=int(notify_dest),
-        train=int(train),
+        train=int(train), engine=int(engine),
     )

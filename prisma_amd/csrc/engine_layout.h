@@ -17,12 +17,13 @@ constexpr uint32_t K_PING = 0u, K_FLOW = 1u, K_COMPLETE = 2u, K_ARRIVE = 3u;
 //            destination, start second, TTL, decision time and -- through the
 //            deciding node and action -- its tunnel are read back from the
 //            decision record in the HBM log)
-//   T_FRESH  data packet of a flow app on its access link: bits 2-10 flow,
-//            bit 11 parity of the start second, bits 12-31 uid mod 2^20
+//   T_FRESH  data packet of a flow app on its access link: bits 2-9 its
+//            destination, bit 10 parity of the start second, bits 11-31 uid
+//            mod 2^21 (its source is the switch it arrives at)
 //   T_PFWD / T_PBACK  ping forward / back (enum-and-constants.h:5-11):
-//            bits 2-9 global tunnel id, bits 10-12 responder position on the
-//            tunnel (ping-backs: 0 = first node after the origin), bits 13-30
-//            round mod 2^18; the one-hop delay a ping-back carries sits in a
+//            bits 2-13 global tunnel id, bits 14-16 responder position on the
+//            tunnel (ping-backs: 0 = first node after the origin), bits 17-30
+//            round mod 2^14; the one-hop delay a ping-back carries sits in a
 //            side table (Layout::s_pbd) keyed by (tunnel, position, round)
 //   echo     small-signalling packet (--train): T_PBACK with bit 31 set,
 //            bits 2-9 = its destination node (the data packet's last hop),
@@ -37,26 +38,27 @@ __host__ __device__ inline uint32_t r_make(uint32_t dec, uint32_t src) {
 }
 __host__ __device__ inline uint32_t r_dec(uint32_t x) { return (x >> 2) & ((1u << 22) - 1u); }
 __host__ __device__ inline uint32_t r_src(uint32_t x) { return x >> 24; }
-__host__ __device__ inline uint32_t f_make(uint32_t flow, uint32_t start_parity, uint32_t uid) {
-    return T_FRESH | (flow << 2) | (start_parity << 11) | (uid << 12);
+__host__ __device__ inline uint32_t f_make(uint32_t dst, uint32_t start_parity, uint32_t uid) {
+    return T_FRESH | (dst << 2) | (start_parity << 10) | (uid << 11);
 }
-__host__ __device__ inline uint32_t f_flow(uint32_t x) { return (x >> 2) & 511u; }
-__host__ __device__ inline uint32_t f_parity(uint32_t x) { return (x >> 11) & 1u; }
-__host__ __device__ inline uint32_t f_uid(uint32_t x) { return x >> 12; }
-constexpr uint32_t kRoundBits = 18u, kRoundMask = (1u << kRoundBits) - 1u;
+__host__ __device__ inline uint32_t f_dst(uint32_t x) { return (x >> 2) & 255u; }
+__host__ __device__ inline uint32_t f_parity(uint32_t x) { return (x >> 10) & 1u; }
+__host__ __device__ inline uint32_t f_uid(uint32_t x) { return x >> 11; }
+constexpr uint32_t kRoundBits = 14u, kRoundMask = (1u << kRoundBits) - 1u;
+constexpr uint32_t kMaxTunnels = 4096u;      // 12-bit tunnel ids in ping entries
 __host__ __device__ inline uint32_t p_make(uint32_t type, uint32_t tunnel, uint32_t pos, uint32_t round) {
-    return type | (tunnel << 2) | (pos << 10) | ((round & kRoundMask) << 13);
+    return type | (tunnel << 2) | (pos << 14) | ((round & kRoundMask) << 17);
 }
-__host__ __device__ inline uint32_t p_tunnel(uint32_t x) { return (x >> 2) & 255u; }
-__host__ __device__ inline uint32_t p_pos(uint32_t x) { return (x >> 10) & 7u; }
-__host__ __device__ inline uint32_t p_round(uint32_t x) { return (x >> 13) & kRoundMask; }
+__host__ __device__ inline uint32_t p_tunnel(uint32_t x) { return (x >> 2) & (kMaxTunnels - 1u); }
+__host__ __device__ inline uint32_t p_pos(uint32_t x) { return (x >> 14) & 7u; }
+__host__ __device__ inline uint32_t p_round(uint32_t x) { return (x >> 17) & kRoundMask; }
 constexpr uint32_t kEchoUidMask = (1u << 21) - 1u;
 __host__ __device__ inline uint32_t e_make(uint32_t uid, uint32_t to) {
     return T_PBACK | kEchoBit | (to << 2) | ((uid & kEchoUidMask) << 10);
 }
 __host__ __device__ inline uint32_t e_uid(uint32_t x) { return (x >> 10) & kEchoUidMask; }
 __host__ __device__ inline uint32_t e_to(uint32_t x) { return (x >> 2) & 255u; }
-constexpr uint32_t kRelayMask = (1u << 22) - 1u, kUidMask = (1u << 20) - 1u;
+constexpr uint32_t kRelayMask = (1u << 22) - 1u, kUidMask = (1u << 21) - 1u;
 
 // pending-notification flags (Hdr::pend_ent[3])
 constexpr uint32_t PEND_DEST = 1u, PEND_ECHO = 2u, PEND_CTRL = 4u;
@@ -141,6 +143,28 @@ struct Layout {
     uint32_t log_cap, rec_bytes;
     double   loss_penalty;
     float    loss_penalty_f;
+    uint32_t pad_lv;
+    // ---- dwords 64..: not in the LV register (read through the scalar cache) ----
+    // memory-resident engine (mem = 1, prisma_engine_mem.hip): the LDS image holds
+    // the header, counters, pending obs and the upper levels of the event tree;
+    // s_ring / s_win / s_pbd are offsets into the HBM part of the state image.
+    uint32_t mem;
+    uint32_t n_leaf, n1, n2;     // event tree: leaves (links, then flows), level-1 / level-2 nodes
+    uint32_t s_lv1, s_lv2;       // LDS offsets of the tree levels (16-B nodes)
+    uint32_t g_lrec, g_keys;     // image offsets of the link records and the leaf keys
+    // topology image offsets (memory-resident engine; variable-size arrays)
+    uint32_t t_rowptr, t_ldst, t_lrev, t_acctx, t_fsrc, t_fdst, t_fmean;
 };
+constexpr uint32_t kLVWords = 64u;           // Layout dwords held in the LV register
+
+// memory-resident engine: one 128-byte record per link (u32 words)
+constexpr uint32_t kLRec = 32u;
+enum : uint32_t {
+    LR_P0 = 0, LR_P1, LR_P2, LR_QB, LR_CPT, LR_CPS, LR_WHT, LR_WHS,
+    LR_PMLO, LR_PMMLO, LR_PMMHI, LR_PMWIN, LR_PAVLO, LR_PAVHI, LR_ODLO, LR_ODHI,
+    LR_WT = 16,                  // wire slots: arrival time (low 32 bits) [8]
+    LR_WS = 24,                  // wire slots: seq [8]
+};
+constexpr uint32_t kMemMaxWire = 8u;
 
 }  // namespace prisma

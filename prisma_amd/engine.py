@@ -17,8 +17,10 @@ from .topology import Topology
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprisma_amd.so")
 
+ABI_VERSION = 6
 PRISMA_POLICY_TABLE = 1
 PRISMA_POLICY_DQN_BUFFER = 2
+PRISMA_ENGINE_AUTO, PRISMA_ENGINE_REGISTER, PRISMA_ENGINE_MEMORY = 0, 1, 2
 
 
 def dqn_buffer_floats(n: int, d: int) -> int:
@@ -46,6 +48,7 @@ class _Params(C.Structure):
         ("ma_size", C.c_uint32), ("ping_as_obs", C.c_uint32), ("auto_reset", C.c_uint32),
         ("loss_penalty", C.c_double), ("seed", C.c_uint64), ("replica_base", C.c_uint32),
         ("log_capacity", C.c_uint32), ("notify_dest", C.c_uint32), ("train", C.c_uint32),
+        ("engine", C.c_uint32),
     ]
 
 
@@ -57,7 +60,7 @@ class _LogView(C.Structure):
 class _Plan(C.Structure):
     _fields_ = [("state_bytes", C.c_uint32), ("lds_bytes", C.c_uint32), ("lds_state_bytes", C.c_uint32),
                 ("ring_entries", C.c_uint32), ("record_bytes", C.c_uint32), ("obs_width", C.c_int32),
-                ("flow_slots", C.c_int32), ("link_slots", C.c_int32)]
+                ("flow_slots", C.c_int32), ("link_slots", C.c_int32), ("engine", C.c_uint32)]
 
 
 EXPORTS = [
@@ -108,7 +111,7 @@ def load_library(path: str = None):
     L.prisma_plan.argtypes = [C.POINTER(_Topo), C.POINTER(_Params), C.POINTER(_Plan)]
     L.prisma_destroy.restype = None
     L.prisma_destroy.argtypes = [C.c_void_p]
-    if L.prisma_abi_version() != 5:
+    if L.prisma_abi_version() != ABI_VERSION:
         raise PrismaError("libprisma_amd ABI version mismatch")
     _lib = L
     return L
@@ -145,11 +148,16 @@ def _topo_struct(topo: Topology):
     return t, keep
 
 
+def _params_struct(params: dict) -> _Params:
+    """prisma_params_t from an engine_params() dict (engine defaults to auto)."""
+    return _Params(**{k: params.get(k, 0) if k == "engine" else params[k] for k, _ in _Params._fields_})
+
+
 def plan(topo: Topology, params: dict) -> dict:
     """prisma_plan: validate a scenario and report its per-replica footprint (no device needed)."""
     L = load_library()
     t, keep = _topo_struct(topo)
-    p = _Params(**{k: params[k] for k, _ in _Params._fields_})
+    p = _params_struct(params)
     out = _Plan()
     _check(L.prisma_plan(C.byref(t), C.byref(p), C.byref(out)))
     return {k: int(getattr(out, k)) for k, _ in _Plan._fields_}
@@ -169,7 +177,7 @@ class PrismaEngine:
         self.device = int(device)
         self.torch_device = torch.device("cuda", self.device)
         t, self._keep = _topo_struct(topo)
-        p = _Params(**{k: params[k] for k, _ in _Params._fields_})
+        p = _params_struct(params)
         h = C.c_void_p()
         with torch.cuda.device(self.device):
             _check(L.prisma_create(C.byref(t), C.byref(p), self.R, self.device, C.byref(h)))
@@ -183,16 +191,21 @@ class PrismaEngine:
         sb, lb = C.c_uint32(), C.c_uint32()
         _check(L.prisma_state_bytes(self.h, C.byref(sb), C.byref(lb)))
         self.state_bytes, self.lds_bytes = int(sb.value), int(lb.value)
-        # register slots of the step-kernel instance the library picked (64 flows / links per slot)
-        fs, ls = 1, 1
-        while 64 * fs < topo.n_flows:
-            fs *= 2
-        while 64 * ls < max(topo.n_links + topo.n_nodes, topo.n_tunnels):
-            ls *= 2
-        tun = "false" if topo.identity else "true"
-        # step-kernel instance (demangled name prefix; the third argument is the in-kernel MLP)
-        self.kernel_name = f"prisma_step_kernel_t<{fs}, {ls}, false, {tun}>"
-        self.kernel_name_mlp = f"prisma_step_kernel_t<{fs}, {ls}, true, {tun}>"
+        # step-kernel instance the library picked (demangled name prefix, for profiles)
+        self.engine_kind = plan(topo, params)["engine"]
+        if self.engine_kind == PRISMA_ENGINE_MEMORY:
+            self.kernel_name = "prisma_mem_step_kernel<false>"
+            self.kernel_name_mlp = "prisma_mem_step_kernel<true>"
+        else:
+            fs, ls = 1, 1                  # register slots per lane (64 flows / links each)
+            while 64 * fs < topo.n_flows:
+                fs *= 2
+            while 64 * ls < max(topo.n_links + topo.n_nodes, topo.n_tunnels):
+                ls *= 2
+            tun = "false" if topo.identity else "true"
+            # the third template argument is the in-kernel MLP
+            self.kernel_name = f"prisma_step_kernel_t<{fs}, {ls}, false, {tun}>"
+            self.kernel_name_mlp = f"prisma_step_kernel_t<{fs}, {ls}, true, {tun}>"
         self.obs = torch.zeros((self.R, self.W), dtype=torch.int32, device=self.torch_device)
         self.mask = torch.zeros(self.R, dtype=torch.uint8, device=self.torch_device)
         self.node = torch.zeros(self.R, dtype=torch.int32, device=self.torch_device)

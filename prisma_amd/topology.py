@@ -444,3 +444,66 @@ def sp_paths(topo: Topology) -> dict:
     lists = _overlay_lists(topo)
     n_o = topo.n_overlay
     return {(u, d): _bidirectional_path(lists, u, d) for u in range(n_o) for d in range(n_o) if u != d}
+
+
+# ----------------------------------------------------------------------
+# Config 5: Erdos-Renyi G(256, 8/255) overlay with a uniform TM.
+# No reference counterpart (the reference's /24 addressing caps it below ~250
+# nodes, sim.cc:443-447); its files are generated once by
+# scripts/make_er256.py into data/er256 and shipped like the other examples.
+# ----------------------------------------------------------------------
+WIRE_BITS_PER_PAYLOAD_BIT = (512 + 30) / 512       # 542-B frames per 512-B payload
+
+
+def erdos_renyi_adjacency(n: int = 256, p: float = 8 / 255, seed: int = 100) -> np.ndarray:
+    """G(n, p) from numpy's PCG64 stream `seed`: the upper triangle is drawn as one
+    n x n uniform matrix per attempt, attempts repeat until the graph is connected."""
+    rng = np.random.default_rng(seed)
+    while True:
+        u = rng.random((n, n))
+        a = np.triu((u < p).astype(np.int32), 1)
+        a = a + a.T
+        seen = np.zeros(n, dtype=bool)
+        seen[0] = True
+        frontier = [0]
+        while frontier:
+            nxt = np.flatnonzero(a[frontier].any(axis=0) & ~seen)
+            seen[nxt] = True
+            frontier = list(nxt)
+        if seen.all() and a.sum(axis=1).min() > 0:
+            return a
+
+
+def sp_link_loads(topo: Topology, rates: np.ndarray, table: np.ndarray) -> np.ndarray:
+    """Wire bits/s offered to every directed link when each pair (s, d) sends
+    rates[s, d] payload bits/s along the SP agent's path (action table)."""
+    load = np.zeros(topo.n_links)
+    n = topo.n_nodes
+    for s in range(n):
+        for d in range(n):
+            if s == d or rates[s, d] <= 0:
+                continue
+            u = s
+            while u != d:
+                l = int(topo.row_ptr[u]) + int(table[u, d])
+                load[l] += rates[s, d] * WIRE_BITS_PER_PAYLOAD_BIT
+                u = int(topo.link_dst[l])
+    return load
+
+
+def erdos_renyi_scenario(n: int = 256, p: float = 8 / 255, seed: int = 100, max_rate_bps: float = 64000.0,
+                         link_cap: int = 500000, max_util: float = 1.0):
+    """(adjacency, integer TM in b/s, SP table): rates U(0, max_rate_bps) per ordered
+    pair (the same PCG64 stream, after the graph), scaled so that the most loaded
+    link carries max_util * link_cap wire bits/s under SP routing, truncated to
+    whole b/s (zero rates create no flow, sim.cc:604)."""
+    adj = erdos_renyi_adjacency(n, p, seed)
+    rng = np.random.default_rng([seed, 1])
+    u = rng.uniform(0.0, max_rate_bps, (n, n))
+    np.fill_diagonal(u, 0.0)
+    unit = Topology.from_matrices(adj, np.ones((n, n), dtype=np.int64) - np.eye(n, dtype=np.int64), name="er")
+    table = sp_next_hop_table(unit)
+    load = sp_link_loads(unit, u, table)
+    scale = max_util * link_cap / load.max()
+    tm = np.floor(u * scale).astype(np.int64)
+    return adj, tm, table

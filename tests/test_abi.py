@@ -32,7 +32,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = engine.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.prisma_abi_version() == 5
+    assert lib.prisma_abi_version() == engine.ABI_VERSION == 6
     out = subprocess.run(["nm", "-D", "--defined-only", engine.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (prisma_\w+)", out))
     assert set(declared_functions()) <= exported
@@ -57,6 +57,7 @@ int main(void) {
   printf("%zu %zu %zu %zu %zu\n", offsetof(prisma_record_t, obs), offsetof(prisma_params_t, loss_penalty),
          offsetof(prisma_params_t, log_capacity), offsetof(prisma_counters_t, cost_sum),
          offsetof(prisma_counters_t, hops_total));
+  printf("%zu %zu %zu\n", offsetof(prisma_params_t, engine), sizeof(prisma_plan_t), offsetof(prisma_plan_t, engine));
   return 0;
 }
 '''
@@ -77,6 +78,8 @@ def test_ctypes_layouts_match_header():
     assert offs[2] == engine._Params.log_capacity.offset
     assert offs[3] == COUNTERS_DTYPE.fields["cost_sum"][1]
     assert offs[4] == COUNTERS_DTYPE.fields["hops_total"][1]
+    eng = list(map(int, lines[2].split()))
+    assert eng == [engine._Params.engine.offset, C.sizeof(engine._Plan), engine._Plan.engine.offset]
 
 
 def test_engine_refuses_without_gpu():
@@ -117,6 +120,35 @@ def test_plan_sizes_and_limits_without_a_device():
     big = Topology.from_matrices(ring, tm)
     with pytest.raises(engine.PrismaError, match="n_nodes"):
         engine.plan(big, engine_params(big))
+
+
+def test_plan_engine_selection():
+    """Auto picks the register-resident engine when the topology fits it, the
+    memory-resident one beyond (256 nodes, > 256 links); either can be forced
+    where it applies."""
+    from prisma_amd.config import engine_params
+    from prisma_amd.topology import Topology
+    ab = Topology.example("abilene")
+    assert engine.plan(ab, engine_params(ab))["engine"] == engine.PRISMA_ENGINE_REGISTER
+    m = engine.plan(ab, engine_params(ab, engine=engine.PRISMA_ENGINE_MEMORY))
+    assert m["engine"] == engine.PRISMA_ENGINE_MEMORY and m["flow_slots"] == 0
+    assert m["obs_width"] == 4 and m["record_bytes"] == 48
+    # 28 + 11 links and 110 flows: 149 leaves -> 3 level-1 nodes, 1 level-2 node in LDS
+    assert m["lds_state_bytes"] == 128 + 160 + 16 + 3 * 16 + 16
+    n = 256
+    ring = np.zeros((n, n), dtype=int)
+    for i in range(n):
+        for d in (1, 2):
+            ring[i, (i + d) % n] = ring[(i + d) % n, i] = 1
+    tm = np.full((n, n), 1000, dtype=object)
+    big = Topology.from_matrices(ring, tm)
+    p = engine.plan(big, engine_params(big))
+    assert p["engine"] == engine.PRISMA_ENGINE_MEMORY
+    with pytest.raises(engine.PrismaError, match="register-resident"):
+        engine.plan(big, engine_params(big, engine=engine.PRISMA_ENGINE_REGISTER))
+    ov = Topology.example("overlay_full_mesh_3n_abilene")
+    with pytest.raises(engine.PrismaError, match="identity overlays"):
+        engine.plan(ov, engine_params(ov, engine=engine.PRISMA_ENGINE_MEMORY))
 
 
 def test_plan_tunnelled_overlay():

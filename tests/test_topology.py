@@ -149,3 +149,23 @@ def test_overlay_example_tunnels_known_answer():
         for d in (0, 2, 4, 5):
             if u != d:
                 assert t.neighbors(u)[table[u, d]] == d
+
+
+def test_er256_config5_files():
+    """BASELINE config 5 data (scripts/make_er256.py): G(256, 8/255) seed 100, connected,
+    identity overlay; the TM loads the busiest SP link to 1.0 of capacity (wire bits,
+    within the truncation to whole b/s); the shipped SP table is the agent's."""
+    from prisma_amd.topology import DATA_DIR, erdos_renyi_adjacency, sp_link_loads
+    topo = Topology.example("er256")
+    assert topo.n_nodes == 256 and topo.identity
+    assert np.array_equal(topo.adjacency, erdos_renyi_adjacency(256, 8 / 255, 100))
+    assert topo.n_links == 2008 and topo.max_deg == 19 and topo.phys_degrees.min() == 1
+    assert topo.n_flows == 65251 and topo.obs_width == 20
+    table = np.load(f"{DATA_DIR}/er256/sp_next_hop_table.npy")
+    rates = np.zeros((256, 256))
+    rates[topo.flow_src, topo.flow_dst] = topo.flow_rate_bps.astype(np.float64)
+    util = sp_link_loads(topo, rates, table) / 500000.0
+    assert 0.999 < util.max() <= 1.0
+    # every table entry is a valid action; following it reaches the destination
+    deg = topo.degrees
+    assert np.all(table < deg[:, None])
