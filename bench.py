@@ -29,7 +29,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "packet-hop transitions/sec at 4096 Abilene replicas; achieved HBM GB/s"   # BASELINE.json
-KERNEL_SOURCES = ["prisma_amd/csrc/prisma_engine.hip", "prisma_amd/csrc/engine_layout.h", "prisma_amd/csrc/numerics.h"]
+KERNEL_SOURCES = ["prisma_amd/csrc/prisma_engine.hip", "prisma_amd/csrc/prisma_engine_mem.hip",
+                  "prisma_amd/csrc/engine_core.h", "prisma_amd/csrc/engine_layout.h", "prisma_amd/csrc/numerics.h"]
 HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
@@ -37,9 +38,12 @@ def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--replicas", type=int, default=4096, help="replicas per GPU")
-    p.add_argument("--hops", type=int, default=2048, help="hops per replica per step")
+    p.add_argument("--warmup", type=int, default=None,
+                   help="untimed steps (default 2; er256: past the first simulated second, whose 65 251 "
+                        "flow-start events are a transient of the episode)")
+    p.add_argument("--replicas", type=int, default=None, help="replicas per GPU (default 4096; er256: 1024 = "
+                                                             "BASELINE config 5's 8192 over 8 GPUs)")
+    p.add_argument("--hops", type=int, default=None, help="hops per replica per step (default 2048; er256: 8192)")
     p.add_argument("--topology", default="abilene")
     p.add_argument("--tm", type=int, default=0)
     p.add_argument("--load-factor", type=float, default=1.0)
@@ -48,7 +52,15 @@ def parse():
                    help="in-kernel policy: DQ-routing argmin table (BASELINE configs[1]), DQN-buffer MLP, SP table")
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-hops", type=int, default=8000000, help="oracle hops per host thread (cpu_baseline)")
-    return p.parse_args()
+    a = p.parse_args()
+    big = a.topology == "er256"
+    if a.replicas is None:
+        a.replicas = 1024 if big else 4096
+    if a.hops is None:
+        a.hops = 8192 if big else 2048
+    if a.warmup is None:
+        a.warmup = 13 if big else 2          # er256: 13 x 8192 hops ~ 1.3 simulated seconds
+    return a
 
 
 def algorithmic_bytes(hops: int, deg_sum: int) -> int:
@@ -137,8 +149,11 @@ def main():
 
     topo = Topology.example(args.topology, args.tm, args.load_factor)
     base, R = shard(args.replicas * world, rank, world)
+    # the decision log must outlive one link crossing (queueing included): ER-256 makes
+    # ~80 k decisions per simulated second against up to ~0.27 s per crossing
+    log_cap = 65536 if topo.n_links > 256 else 8192
     params = engine_params(topo, sim_time_s=60.0, ping_as_obs=args.ping_as_obs, auto_reset=1,
-                           replica_base=base, seed=100)
+                           replica_base=base, seed=100, log_capacity=log_cap)
     eng = PrismaEngine(topo, params, R, device=local)
     if args.policy == "dqn_buffer":
         agent = StackedQNet(topo, "buffer", seed=1234, device=dev)

@@ -45,7 +45,7 @@ static __device__ unsigned int g_prisma_trace_cap;
 static __device__ unsigned int g_prisma_trace_n[8];
 #endif
 #if PRISMA_TIMING
-__device__ unsigned long long g_prisma_timing[16];
+static __device__ unsigned long long g_prisma_timing[16];   // one copy per engine (translation unit)
 #define TM_NOW() ((uint64_t)__builtin_amdgcn_s_memtime())
 #endif
 
@@ -399,6 +399,7 @@ struct LinkV {
     uint32_t head, txp, tail, n_wire, n_queue, busy, qb;
     uint32_t cp_t, cp_seq;       // completion time (low 32 bits), seq
     uint32_t wh_t, wh_seq;       // wire-head arrival time (low 32 bits), seq
+    uint32_t rec;                // memory-resident engine: the link's record, lane j = word j
 };
 
 template <int FS, int LS>
@@ -481,12 +482,34 @@ __device__ __forceinline__ void ping_set_win(const Sim& S, Regs<FS, LS>& R, uint
     R.pav_hi.set(t, (uint32_t)(avg >> 32));
 }
 
-// wire slot i of link l: arrival time (low 32 bits) and seq
-__device__ __forceinline__ uint32_t* wire_t(const Sim& S, uint32_t l, uint32_t i) {
-    return S.mem ? S.lrec + l * kLRec + LR_WT + i : S.wt + l * (uint32_t)S.lv.WCAP() + i;
+// Wire slot i of link l: arrival time (low 32 bits), seq and -- memory-resident
+// engine -- the packet entry.  Register-resident: LDS arrays; memory-resident: words
+// LR_WT + {i, WCAP + i, 2 WCAP + i} of the link record held in k.rec (written back by
+// link_put), so an arrival reads its packet without a ring access.
+__device__ __forceinline__ void wire_set(const Sim& S, LinkV& k, uint32_t l, uint32_t i, uint32_t t, uint32_t s,
+                                         uint32_t x) {
+    const uint32_t W = (uint32_t)S.lv.WCAP();
+    if (S.mem) {
+        const uint32_t j = (uint32_t)S.lane;
+        k.rec = j == LR_WT + i ? t : (j == LR_WT + W + i ? s : (j == LR_WT + 2u * W + i ? x : k.rec));
+    } else if (S.lane == 0) {
+        S.wt[l * W + i] = t;
+        S.wseq[l * W + i] = s;
+    }
 }
-__device__ __forceinline__ uint32_t* wire_s(const Sim& S, uint32_t l, uint32_t i) {
-    return S.mem ? S.lrec + l * kLRec + LR_WS + i : S.wseq + l * (uint32_t)S.lv.WCAP() + i;
+__device__ __forceinline__ void wire_get(const Sim& S, const LinkV& k, uint32_t l, uint32_t i, uint32_t& t,
+                                         uint32_t& s) {
+    const uint32_t W = (uint32_t)S.lv.WCAP();
+    if (S.mem) {
+        t = rdl(k.rec, LR_WT + i);
+        s = rdl(k.rec, LR_WT + W + i);
+    } else {
+        t = u_ld32(S.wt + l * W + i);
+        s = u_ld32(S.wseq + l * W + i);
+    }
+}
+__device__ __forceinline__ uint32_t wire_ent(const Sim& S, const LinkV& k, uint32_t i) {
+    return rdl(k.rec, LR_WT + 2u * (uint32_t)S.lv.WCAP() + i);
 }
 
 // ---- link FIFO / transmitter (point-to-point-net-device.cc:273-336, 595-666)
@@ -503,8 +526,7 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
     const uint32_t w = ring_idx & (uint32_t)(L.WCAP() - 1);
     const uint32_t at = lo32(H.now + tx + prop);
     const uint32_t as = H.seq++;                               // channel Receive
-    st_rep(S, wire_t(S, l, w), at);
-    st_rep(S, wire_s(S, l, w), as);
+    wire_set(S, k, l, w, at, as, x);
     if (k.n_wire == 1) { k.wh_t = at; k.wh_seq = as; }        // the wire was empty: new head
     if (k.n_wire > (uint32_t)L.WCAP()) fail(H, PRISMA_EBIT_WIRE);
 }
@@ -907,8 +929,7 @@ __device__ __forceinline__ void wire_pop(const Sim& S, RS& R, const Hot& H, uint
     k.n_wire--;
     if (k.n_wire) {                                                 // next packet on the wire
         const uint32_t w = k.head & (uint32_t)(L.WCAP() - 1);
-        k.wh_t = u_ld32(wire_t(S, l, w));
-        k.wh_seq = u_ld32(wire_s(S, l, w));
+        wire_get(S, k, l, w, k.wh_t, k.wh_seq);
     }
     link_put(S, R, H, l, k);
 }
@@ -991,10 +1012,11 @@ __device__ __forceinline__ uint32_t pbd_slot(const Sim& S, uint32_t t, uint32_t 
 template <class RS>
 __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l, Decision& D, bool fused) {
     const LV& L = S.lv;
-    LinkV k = link_get(R, l);
-    const uint32_t x = u_ld32(&S.ring[ring_off(S, l) + k.head]);
-    const uint32_t type = ent_type(x);
     const uint32_t v = (uint32_t)t_ldst(S, l);
+    LinkV k = link_get(R, l);
+    const uint32_t x = S.mem ? wire_ent(S, k, k.head & (uint32_t)(L.WCAP() - 1))
+                             : u_ld32(&S.ring[ring_off(S, l) + k.head]);
+    const uint32_t type = ent_type(x);
     const bool tun = S.tun;
     if (ent_is_data(x)) {
         // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
@@ -1011,6 +1033,10 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap() - 1)) * L.rec_bytes();
         const uint4 ph = *(const uint4*)pr;
         const uint2 pw = *(const uint2*)(pr + 24);
+        // memory-resident engine: the observation's gather goes out with the record
+        // load, before the arrival link's update (it reads node v's out-links, which
+        // nothing touches before the decision)
+        const uint32_t obs_early = S.mem ? observe_links(S, R, H, v, ns_to_sec(H.now)) : 0u;
         wire_pop(S, R, H, l, k);
         uint32_t ttl = 255u;                                        // SetIpTtl(255) (poisson-application.cc:330)
         if (tun && type == T_RELAY) {
@@ -1046,7 +1072,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
             ttl = ttl_prev - (ti_len(ti) - 1u);
         }
         H.dec = d + 1u;
-        const uint32_t obs_links = observe_links(S, R, H, v, ns_to_sec(H.now));
+        const uint32_t obs_links = S.mem ? obs_early : observe_links(S, R, H, v, ns_to_sec(H.now));
         const int64_t t_prev = mk64(rfl(ph.x), rfl(ph.y));
         const uint32_t uid_prev = rfl(ph.z), w_prev = rfl(pw.x);
         double reward = 0.0;

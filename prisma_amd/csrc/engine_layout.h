@@ -151,20 +151,21 @@ struct Layout {
     uint32_t mem;
     uint32_t n_leaf, n1, n2;     // event tree: leaves (links, then flows), level-1 / level-2 nodes
     uint32_t s_lv1, s_lv2;       // LDS offsets of the tree levels (16-B nodes)
-    uint32_t g_lrec, g_keys;     // image offsets of the link records and the leaf keys
+    uint32_t g_lrec, g_keys;     // image offsets of the link records and the flow leaf keys
+    uint32_t lrec_words;         // words per link record (32 or 64)
+    uint32_t s_lkey, s_lkind;    // LDS offsets of the link leaf keys (time lo, seq) and kinds (bytes)
     // topology image offsets (memory-resident engine; variable-size arrays)
     uint32_t t_rowptr, t_ldst, t_lrev, t_acctx, t_fsrc, t_fdst, t_fmean;
 };
 constexpr uint32_t kLVWords = 64u;           // Layout dwords held in the LV register
 
-// memory-resident engine: one 128-byte record per link (u32 words)
-constexpr uint32_t kLRec = 32u;
+// memory-resident engine: one record of Layout::lrec_words (32 or 64) u32 words per
+// link, accessed lane j <-> word j (one coalesced load / masked store per access)
 enum : uint32_t {
     LR_P0 = 0, LR_P1, LR_P2, LR_QB, LR_CPT, LR_CPS, LR_WHT, LR_WHS,
     LR_PMLO, LR_PMMLO, LR_PMMHI, LR_PMWIN, LR_PAVLO, LR_PAVHI, LR_ODLO, LR_ODHI,
-    LR_WT = 16,                  // wire slots: arrival time (low 32 bits) [8]
-    LR_WS = 24,                  // wire slots: seq [8]
+    LR_WT = 16,                  // wire slots: arrival time [WCAP], seq [WCAP], packet entry [WCAP]
 };
-constexpr uint32_t kMemMaxWire = 8u;
+constexpr uint32_t kMemMaxWire = 16u;
 
 }  // namespace prisma

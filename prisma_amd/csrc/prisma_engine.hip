@@ -318,13 +318,15 @@ static int plan_overlay(const prisma_topology_t* T, OverlayPlan& OP) {
 
 // Memory-resident engine (prisma_engine_mem.hip, identity overlays): topology as
 // variable-size arrays; state image = LDS part (header, counters, pending obs,
-// event-tree levels 1-2) + HBM part (link records, leaf keys, rings, ping windows,
-// ping-back delays).  Scenario constants and ring sizing are set by build_layout.
+// event-tree levels 1-2, link leaf keys) + HBM part (link records, flow leaf keys,
+// rings, ping windows, ping-back delays).  Scenario constants and ring sizing are set
+// by build_layout.
 static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layout& L,
                       std::vector<unsigned char>& topo, const std::vector<int64_t>& acctx,
                       const std::vector<int32_t>& ldst, uint32_t ring_total) {
     const int N = T->n_nodes, E = T->n_links, F = T->n_flows, Lk = E + N;
-    if (L.WCAP > (int)kMemMaxWire) return set_err(PRISMA_ERR_CONFIG, "more than 8 packets on a wire (memory-resident engine)");
+    if (L.WCAP > (int)kMemMaxWire) return set_err(PRISMA_ERR_CONFIG, "more than 16 packets on a wire (memory-resident engine)");
+    L.lrec_words = LR_WT + 3u * (uint32_t)L.WCAP <= 32u ? 32u : 64u;
     const uint64_t n_leaf = (uint64_t)Lk + (uint64_t)F;
     if (n_leaf > 64ull * 64ull * 64ull) return set_err(PRISMA_ERR_CONFIG, "more than 262 144 links + flows per replica");
     L.mem = 1;
@@ -360,9 +362,11 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
         return set_err(PRISMA_ERR_CONFIG, "internal: LDS header offsets");
     L.s_lv1 = take(16u * L.n1);
     L.s_lv2 = take(16u * L.n2);
+    L.s_lkey = take(8u * (uint64_t)Lk);
+    L.s_lkind = take((uint64_t)Lk);
     L.lds_state_bytes = (uint32_t)o;
-    L.g_lrec = take(4u * kLRec * (uint64_t)Lk);
-    L.g_keys = take(16u * n_leaf);
+    L.g_lrec = take(4u * L.lrec_words * (uint64_t)Lk);
+    L.g_keys = take(16u * (uint64_t)F);
     L.s_ring = take(4u * (uint64_t)ring_total);
     L.s_win = take(4u * (uint64_t)E * L.MA);
     L.s_pbd = take(4u * (uint64_t)E * L.PBK);

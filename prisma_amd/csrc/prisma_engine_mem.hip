@@ -23,11 +23,13 @@
 // store
 // ---------------------------------------------------------------------------
 struct MemSt {
-    uint32_t* lrec;              // [L][kLRec]
-    uint4* keys;                 // [n_leaf] {t lo, t hi, seq, aux}: aux = kind (links) / draw (flows)
+    uint32_t* lrec;              // [L][RW] link records (HBM)
+    uint4* fkeys;                // [F] flow leaf keys {t lo, t hi, seq, draw} (HBM)
+    uint2* lkey;                 // LDS [L] link leaf keys {t lo, seq}: t = now + (t lo - lo32(now))
+    uint8_t* lkind;              // LDS [L] link event kind (0: none, K_COMPLETE, K_ARRIVE)
     uint4* lv1;                  // LDS [n1] {t lo, t hi, seq, code}
     uint4* lv2;                  // LDS [n2]
-    uint32_t L, n_leaf, n1, n2;
+    uint32_t L, n_leaf, n1, n2, RW, WCAP;
 };
 
 constexpr int64_t kInf = INT64_MAX;
@@ -68,16 +70,24 @@ __device__ __forceinline__ void lds_put_key(const Sim& S, uint4* p, const Key& k
     if (S.lane == 0) *p = make_uint4(lo32(k.t), hi32(k.t), k.s, k.c);
 }
 
-// minimum of leaf block b (64 leaves, one per lane)
-__device__ __forceinline__ Key block_min(const Sim& S, const MemSt& R, uint32_t b) {
+// minimum of leaf block b (64 leaves, one per lane): links from LDS, flows from HBM
+__device__ __forceinline__ Key block_min(const Sim& S, const MemSt& R, uint32_t b, int64_t now) {
     const uint32_t leaf = b * 64u + (uint32_t)S.lane;
     int64_t t = kInf;
     uint32_t s = 0xffffffffu, c = 0u;
-    if (leaf < R.n_leaf) {
-        const uint4 k = R.keys[leaf];
+    if (leaf < R.L) {
+        const uint2 k = R.lkey[leaf];
+        const uint32_t kind = R.lkind[leaf];
+        if (kind) {
+            t = now + (int64_t)(uint32_t)(k.x - lo32(now));
+            s = k.y;
+        }
+        c = (kind << 28) | leaf;
+    } else if (leaf < R.n_leaf) {
+        const uint4 k = R.fkeys[leaf - R.L];
         t = mk64(k.x, k.y);
         s = k.z;
-        c = leaf < R.L ? ((k.w << 28) | leaf) : ((K_FLOW << 28) | (leaf - R.L));
+        c = (K_FLOW << 28) | (leaf - R.L);
     }
     return wave_min_key(t, s, c);
 }
@@ -95,19 +105,26 @@ __device__ __forceinline__ Key group_min(const Sim& S, const MemSt& R, uint32_t 
     return wave_min_key(t, s, c);
 }
 
-// A source's next event changed to (t, seq): store the leaf key and repair the
-// two tree levels above it.  A block is re-reduced only if the leaf was its
-// minimum and did not become smaller; a new smaller key just replaces it.
-__device__ __forceinline__ void tree_touch(const Sim& S, MemSt& R, uint32_t leaf, int64_t t, uint32_t seq,
-                                           uint32_t code, uint32_t aux) {
-    st_rep(S, &R.keys[leaf], make_uint4(lo32(t), hi32(t), seq, aux));
+// Source `leaf`'s next event changed to (t, seq): store its key and repair the two
+// tree levels above it.  A block is re-reduced only if the leaf was its minimum and
+// did not become smaller; a new smaller key just replaces it.
+__device__ __forceinline__ void tree_touch(const Sim& S, MemSt& R, const Hot& H, uint32_t leaf, int64_t t,
+                                           uint32_t seq, uint32_t code, uint32_t aux) {
+    if (leaf < R.L) {
+        if (S.lane == 0) {
+            R.lkey[leaf] = make_uint2(lo32(t), seq);
+            R.lkind[leaf] = (uint8_t)aux;
+        }
+    } else {
+        st_rep(S, &R.fkeys[leaf - R.L], make_uint4(lo32(t), hi32(t), seq, aux));
+    }
     const uint32_t b = leaf >> 6;
     const Key cur = lds_key(&R.lv1[b]);
     Key nb;
     if (key_less(t, seq, cur.t, cur.s)) {
         nb.t = t; nb.s = seq; nb.c = code;
     } else if (leaf_of(R, cur.c) == leaf) {
-        nb = block_min(S, R, b);
+        nb = block_min(S, R, b, H.now);
     } else {
         return;
     }
@@ -125,29 +142,42 @@ __device__ __forceinline__ void tree_touch(const Sim& S, MemSt& R, uint32_t leaf
     lds_put_key(S, &R.lv2[g], ng);
 }
 
-// ---- links: words 0-7 of the 128-B record, read and written by every lane as
-// two 16-B accesses (each lane's later reads follow its own stores) ----
+// ---- links: the whole record is one coalesced load (lane j: word j) and the fields
+// come out with v_readlane; a write-back stores words 0-7 and the wire slots (lane j
+// writes word j), so every word is only ever read and written by its own lane ----
+__device__ __forceinline__ uint32_t rec_load(const MemSt& R, uint32_t l) {
+    const uint32_t j = threadIdx.x;
+    return j < R.RW ? R.lrec[l * R.RW + j] : 0u;
+}
+
 __device__ __forceinline__ LinkV link_get(const MemSt& R, uint32_t l) {
-    const uint4* p = (const uint4*)(R.lrec + l * kLRec);
-    const uint4 a = p[0], b = p[1];
     LinkV k;
-    const uint32_t p0 = rfl(a.x), p1 = rfl(a.y), p2 = rfl(a.z);
+    k.rec = rec_load(R, l);
+    const uint32_t p0 = rdl(k.rec, LR_P0), p1 = rdl(k.rec, LR_P1), p2 = rdl(k.rec, LR_P2);
     k.head = p0 & 0xffffu; k.txp = p0 >> 16;
     k.tail = p1 & 0xffffu; k.n_wire = p1 >> 16;
     k.n_queue = p2 & 0xffffu; k.busy = p2 >> 16;
-    k.qb = rfl(a.w);
-    k.cp_t = rfl(b.x);
-    k.cp_seq = rfl(b.y);
-    k.wh_t = rfl(b.z);
-    k.wh_seq = rfl(b.w);
+    k.qb = rdl(k.rec, LR_QB);
+    k.cp_t = rdl(k.rec, LR_CPT);
+    k.cp_seq = rdl(k.rec, LR_CPS);
+    k.wh_t = rdl(k.rec, LR_WHT);
+    k.wh_seq = rdl(k.rec, LR_WHS);
     return k;
 }
 
 __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, uint32_t l, const LinkV& k) {
-    uint4* p = (uint4*)(R.lrec + l * kLRec);
-    p[0] = make_uint4(k.head | (k.txp << 16), k.tail | (k.n_wire << 16), k.n_queue | (k.busy << 16), k.qb);
-    p[1] = make_uint4(k.cp_t, k.cp_seq, k.wh_t, k.wh_seq);
-    // next event of the link (register-resident link_put's rule), as an absolute key
+    const uint32_t j = threadIdx.x;
+    uint32_t w = k.rec;
+    w = j == LR_P0 ? (k.head | (k.txp << 16)) : w;
+    w = j == LR_P1 ? (k.tail | (k.n_wire << 16)) : w;
+    w = j == LR_P2 ? (k.n_queue | (k.busy << 16)) : w;
+    w = j == LR_QB ? k.qb : w;
+    w = j == LR_CPT ? k.cp_t : w;
+    w = j == LR_CPS ? k.cp_seq : w;
+    w = j == LR_WHT ? k.wh_t : w;
+    w = j == LR_WHS ? k.wh_seq : w;
+    if (j < LR_PMLO || (j >= LR_WT && j < LR_WT + 3u * R.WCAP)) R.lrec[l * R.RW + j] = w;
+    // next event of the link (register-resident link_put's rule)
     const uint32_t n0 = lo32(H.now);
     uint32_t t = 0, s = 0xffffffffu, kind = 0;
     if (k.busy) { t = k.cp_t; s = k.cp_seq; kind = K_COMPLETE; }
@@ -156,50 +186,51 @@ __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, u
         if (kind == 0 || rw < rt || (rw == rt && k.wh_seq < s)) { t = k.wh_t; s = k.wh_seq; kind = K_ARRIVE; }
     }
     const int64_t at = kind ? H.now + (int64_t)(uint32_t)(t - n0) : kInf;
-    tree_touch(S, R, l, at, s, (kind << 28) | l, kind);
+    tree_touch(S, R, H, l, at, s, (kind << 28) | l, kind);
 }
 
 // ---- flows ----
 __device__ __forceinline__ uint32_t flow_draw(const Sim& S, const MemSt& R, uint32_t f) {
-    return u_ld32(&R.keys[R.L + f].w);
+    return u_ld32(&R.fkeys[f].w);
 }
 __device__ __forceinline__ void flow_set(const Sim& S, MemSt& R, const Hot& H, uint32_t f, int64_t t, uint32_t seq,
                                          uint32_t draw) {
-    tree_touch(S, R, R.L + f, t, seq, (K_FLOW << 28) | f, draw);
+    tree_touch(S, R, H, R.L + f, t, seq, (K_FLOW << 28) | f, draw);
 }
 
-// ---- ping state of tunnel t (== link t: identity overlays only) ----
+// ---- ping state of tunnel t (== link t: identity overlays only), words 8-15 ----
 __device__ __forceinline__ PingV ping_get(const Sim& S, const MemSt& R, uint32_t t) {
-    const uint4 w = *(const uint4*)(R.lrec + t * kLRec + LR_PMLO);
+    const uint32_t w = rec_load(R, t);
     PingV p;
-    p.lo = rfl(w.x); p.mlo = rfl(w.y); p.mhi = rfl(w.z); p.win = rfl(w.w);
+    p.lo = rdl(w, LR_PMLO); p.mlo = rdl(w, LR_PMMLO); p.mhi = rdl(w, LR_PMMHI); p.win = rdl(w, LR_PMWIN);
     return p;
 }
+__device__ __forceinline__ void rec_put2(const MemSt& R, uint32_t t, uint32_t w0, uint32_t a, uint32_t b) {
+    const uint32_t j = threadIdx.x;
+    if (j == w0 || j == w0 + 1u) R.lrec[t * R.RW + j] = j == w0 ? a : b;
+}
 __device__ __forceinline__ void ping_set_lo(const Sim& S, MemSt& R, uint32_t t, uint32_t lo, uint64_t od) {
-    uint32_t* p = R.lrec + t * kLRec;
-    p[LR_PMLO] = lo;
-    p[LR_ODLO] = (uint32_t)od;
-    p[LR_ODHI] = (uint32_t)(od >> 32);
+    const uint32_t j = threadIdx.x;
+    if (j == LR_PMLO || j == LR_ODLO || j == LR_ODHI)
+        R.lrec[t * R.RW + j] = j == LR_PMLO ? lo : (j == LR_ODLO ? (uint32_t)od : (uint32_t)(od >> 32));
 }
 __device__ __forceinline__ void ping_set_mask(const Sim& S, MemSt& R, uint32_t t, uint64_t mask) {
-    uint32_t* p = R.lrec + t * kLRec;
-    p[LR_PMMLO] = (uint32_t)mask;
-    p[LR_PMMHI] = (uint32_t)(mask >> 32);
+    rec_put2(R, t, LR_PMMLO, (uint32_t)mask, (uint32_t)(mask >> 32));
 }
 __device__ __forceinline__ void ping_set_win(const Sim& S, MemSt& R, uint32_t t, uint32_t win, uint64_t avg) {
-    uint32_t* p = R.lrec + t * kLRec;
-    p[LR_PMWIN] = win;
-    p[LR_PAVLO] = (uint32_t)avg;
-    p[LR_PAVHI] = (uint32_t)(avg >> 32);
+    const uint32_t j = threadIdx.x;
+    if (j == LR_PMWIN || j == LR_PAVLO || j == LR_PAVHI)
+        R.lrec[t * R.RW + j] = j == LR_PMWIN ? win : (j == LR_PAVLO ? (uint32_t)avg : (uint32_t)(avg >> 32));
 }
 
-// observation of node v: lane i (1 <= i <= deg) evaluates link ovrow[v] + i - 1
+// observation of node v: lane i (1 <= i <= deg) gathers the words of link ovrow[v] + i - 1
+// (written by other lanes of this wave in earlier events)
 __device__ __forceinline__ uint32_t observe_links(const Sim& S, const MemSt& R, const Hot& H, uint32_t v,
                                                   double now_s) {
     const int r0 = t_ovrow(S, v), deg = t_ovrow(S, v + 1) - r0;
     const int lane = S.lane;
     if (lane < 1 || lane > deg) return 0u;
-    const uint32_t* p = R.lrec + (uint32_t)(r0 + lane - 1) * kLRec;
+    const uint32_t* p = R.lrec + (uint32_t)(r0 + lane - 1) * R.RW;
     if (S.lv.ping_as_obs())
         return ping_value_lane(ld_d(p[LR_PAVLO], p[LR_PAVHI]), p[LR_PMLO], ld_d(p[LR_ODLO], p[LR_ODHI]),
                                H.ping_rounds, now_s);
@@ -247,13 +278,17 @@ __device__ __forceinline__ void mem_bind(Sim& S, MemSt& R, const KParams& P, con
     S.m_fdst = (const CAS int32_t*)(tb + LC.t_fdst);
     S.m_fmean = (const CAS double*)(tb + LC.t_fmean);
     R.lrec = S.lrec;
-    R.keys = (uint4*)(img + LC.g_keys);
+    R.fkeys = (uint4*)(img + LC.g_keys);
+    R.lkey = (uint2*)(lds + LC.s_lkey);
+    R.lkind = (uint8_t*)(lds + LC.s_lkind);
     R.lv1 = (uint4*)(lds + LC.s_lv1);
     R.lv2 = (uint4*)(lds + LC.s_lv2);
     R.L = (uint32_t)LC.L;
     R.n_leaf = LC.n_leaf;
     R.n1 = LC.n1;
     R.n2 = LC.n2;
+    R.RW = LC.lrec_words;
+    R.WCAP = (uint32_t)LC.WCAP;
 }
 
 // episode start (sim.cc:610-630, data-packet-manager.cc:118-121): LDS header,
@@ -270,28 +305,25 @@ __device__ __forceinline__ void init_replica(Sim& S, MemSt& R, Hot& H, uint32_t 
     for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes() / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
     const uint64_t od = (uint64_t)__double_as_longlong(ping_send_s(L, 0));
     const uint32_t NL = R.L;
-    for (uint32_t i = (uint32_t)lane; i < NL * 16u; i += kWave) {          // words 0..15 of every record
-        const uint32_t l = i >> 4, w = i & 15u;
-        const uint32_t v = w == LR_ODLO ? (uint32_t)od : (w == LR_ODHI ? (uint32_t)(od >> 32) : 0u);
-        R.lrec[l * kLRec + w] = v;
+    const uint32_t j = (uint32_t)lane;
+    if (j < R.RW) {                                   // lane j writes word j of every record
+        const uint32_t v = j == LR_ODLO ? (uint32_t)od : (j == LR_ODHI ? (uint32_t)(od >> 32) : 0u);
+        for (uint32_t l = 0; l < NL; ++l) R.lrec[l * R.RW + j] = v;
     }
-    for (uint32_t i = (uint32_t)lane; i < R.n_leaf; i += kWave) {
-        uint4 k;
-        if (i < NL) {
-            k = make_uint4(lo32(kInf), hi32(kInf), 0xffffffffu, 0u);
-        } else {
-            const uint32_t f = i - NL;
-            uint32_t c[4] = { f, 0u, episode, 0u };
-            philox4x32_10(c, L.seed_lo(), S.gid);
-            uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
-            double U = (double)u53 * (1.0 / 9007199254740992.0);
-            const int64_t t = sec_to_ns(0.0001 + U);
-            k = make_uint4(lo32(t), hi32(t), (uint32_t)L.NO() + f, 0u);  // after the NO ping timers
-        }
-        R.keys[i] = k;
+    // flow leaves (link leaves are in LDS, zeroed: no event); lane j writes the leaves
+    // 64b + j that its block reductions read back
+    for (uint32_t i = j; i < R.n_leaf; i += kWave) {
+        if (i < NL) continue;
+        const uint32_t f = i - NL;
+        uint32_t c[4] = { f, 0u, episode, 0u };
+        philox4x32_10(c, L.seed_lo(), S.gid);
+        uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
+        double U = (double)u53 * (1.0 / 9007199254740992.0);
+        const int64_t t = sec_to_ns(0.0001 + U);                 // sim.cc:610-630
+        R.fkeys[f] = make_uint4(lo32(t), hi32(t), (uint32_t)L.NO() + f, 0u);   // after the NO ping timers
     }
-    // leaf 64b + lane was written by this lane above: block_min reads its own stores
-    for (uint32_t b = 0; b < R.n1; ++b) lds_put_key(S, &R.lv1[b], block_min(S, R, b));
+    __syncthreads();
+    for (uint32_t b = 0; b < R.n1; ++b) lds_put_key(S, &R.lv1[b], block_min(S, R, b, 0));
     __syncthreads();
     for (uint32_t g = 0; g < R.n2; ++g) lds_put_key(S, &R.lv2[g], group_min(S, R, g));
     H.now = 0;
@@ -381,5 +413,15 @@ extern "C" int prisma_debug_trace(void* dev_buf, unsigned int cap) {
     return (hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_trace), &dev_buf, sizeof(void*)) == hipSuccess &&
             hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_trace_cap), &cap, sizeof(cap)) == hipSuccess &&
             hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_trace_n), z, sizeof(z)) == hipSuccess) ? 0 : -1;
+}
+#endif
+
+#if PRISMA_TIMING
+// diagnostic build only: read and clear the memory-resident engine's per-phase cycle totals
+extern "C" int prisma_debug_timing_mem(unsigned long long* out16) {
+    if (hipDeviceSynchronize() != hipSuccess ||
+        hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prisma_timing), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    unsigned long long z[16] = {0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

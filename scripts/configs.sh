@@ -1,7 +1,8 @@
 #!/bin/bash
 # One bench line per BASELINE.json config that fits one GPU, appended to
 # gpurun_out/configs.jsonl.  Config 4 runs its per-GPU share (16384 / 8 = 2048 replicas)
-# across the load-factor sweep; config 5 (ER-256) is not supported by this engine.
+# across the load-factor sweep; config 5 (ER-256, memory-resident engine) its per-GPU share
+# (8192 / 8 = 1024 replicas).
 set -e
 OUT=gpurun_out/configs.jsonl
 : > $OUT
@@ -13,6 +14,8 @@ echo "config 3 (SP table)" && $B --topology abilene_on_geant --policy sp >> $OUT
 for lf in 0.5 0.75 1.0 1.25 1.5 1.75 2.0; do
   echo "config 4: geant DQN-buffer pingAsObs=0 lf $lf, 2048" && $B --topology geant --policy dqn_buffer --ping-as-obs 0 --load-factor $lf --replicas 2048 --hops 1024 >> $OUT
 done
+echo "config 5: ER-256 DQN-buffer pingAsObs=1, 1024" && $B --topology er256 --policy dqn_buffer --replicas 1024 --hops 512 >> $OUT
+echo "config 5 (SP table)" && $B --topology er256 --policy sp --replicas 1024 --hops 2048 >> $OUT
 python - <<'PY'
 import json
 for l in open("gpurun_out/configs.jsonl"):

@@ -15,9 +15,14 @@ NAMES = ["select", "arrive", "decision", "complete", "flow", "ping_round", "dec:
 
 if sys.argv[1] == "build":
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC",
-                           "-shared", "-std=c++17", "-DPRISMA_TIMING=1", "-o", LIB,
-                           os.path.join(ROOT, "prisma_amd", "csrc", "prisma_engine.hip")])
+    objs = []
+    for f in ("prisma_engine.hip", "prisma_engine_mem.hip"):
+        o = os.path.join(os.path.dirname(LIB), f + ".timing.o")
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC",
+                               "-std=c++17", "-DPRISMA_TIMING=1", "-c", "-o", o,
+                               os.path.join(ROOT, "prisma_amd", "csrc", f)])
+        objs.append(o)
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB, *objs])
     sys.exit(0)
 
 os.environ["PRISMA_LIB"] = LIB
@@ -30,19 +35,24 @@ from prisma_amd.topology import Topology  # noqa: E402
 
 topo_name = sys.argv[sys.argv.index("--topology") + 1] if "--topology" in sys.argv else "abilene"
 R = int(sys.argv[sys.argv.index("--replicas") + 1]) if "--replicas" in sys.argv else 4096
+HOPS = int(sys.argv[sys.argv.index("--hops") + 1]) if "--hops" in sys.argv else 2048
 topo = Topology.example(topo_name)
-eng = PrismaEngine(topo, engine_params(topo, sim_time_s=60.0, ping_as_obs=1, auto_reset=1), R)
+eng = PrismaEngine(topo, engine_params(topo, sim_time_s=60.0, ping_as_obs=1, auto_reset=1,
+                                      log_capacity=65536 if topo.n_links > 256 else 8192), R)
 lib = load_library()
-lib.prisma_debug_timing.argtypes = [C.c_void_p]
+timing = lib.prisma_debug_timing_mem if eng.engine_kind == 2 else lib.prisma_debug_timing
+timing.argtypes = [C.c_void_p]
 table = StackedQNet(topo, "routing", seed=1234).argmin_table()
 eng.reset(0)
-eng.run(table, 2048)
+WARM = int(sys.argv[sys.argv.index("--warm") + 1]) if "--warm" in sys.argv else 1
+for _ in range(WARM):
+    eng.run(table, HOPS)
 buf = (C.c_ulonglong * 16)()
-lib.prisma_debug_timing(buf)
+timing(buf)
 h0 = int(eng.counters()["hops_total"].sum())
 for _ in range(4):
-    eng.run(table, 2048)
-lib.prisma_debug_timing(buf)
+    eng.run(table, HOPS)
+timing(buf)
 hops = int(eng.counters()["hops_total"].sum()) - h0
 tot = sum(buf[i] for i in range(8))
 print(f"{topo_name} R={R}: cycles/hop/wave = {tot / max(1, hops):.0f}")

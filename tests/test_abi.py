@@ -133,8 +133,9 @@ def test_plan_engine_selection():
     m = engine.plan(ab, engine_params(ab, engine=engine.PRISMA_ENGINE_MEMORY))
     assert m["engine"] == engine.PRISMA_ENGINE_MEMORY and m["flow_slots"] == 0
     assert m["obs_width"] == 4 and m["record_bytes"] == 48
-    # 28 + 11 links and 110 flows: 149 leaves -> 3 level-1 nodes, 1 level-2 node in LDS
-    assert m["lds_state_bytes"] == 128 + 160 + 16 + 3 * 16 + 16
+    # 28 + 11 links and 110 flows: 149 leaves -> 3 level-1 nodes, 1 level-2 node, and the
+    # 39 link leaf keys (8 B) and kinds (1 B) in LDS, each region 16-B aligned
+    assert m["lds_state_bytes"] == 128 + 160 + 16 + 3 * 16 + 16 + 320 + 48
     n = 256
     ring = np.zeros((n, n), dtype=int)
     for i in range(n):
