@@ -118,9 +118,10 @@ def pmc_traffic(topology: str, replicas: int, hops: int):
     try:
         with open(path) as fh:
             d = json.load(fh)
-        if (d.get("topology") == topology and int(d.get("replicas", -1)) == replicas
-                and int(d.get("hops", -1)) == hops and d.get("kernel_source") == kernel_source_hash()):
-            return float(d["bytes_per_launch"])
+        for e in d.get("entries", [d]):
+            if (e.get("topology") == topology and int(e.get("replicas", -1)) == replicas
+                    and int(e.get("hops", -1)) == hops and e.get("kernel_source") == kernel_source_hash()):
+                return float(e["bytes_per_launch"])
     except (OSError, ValueError, KeyError):
         pass
     return None

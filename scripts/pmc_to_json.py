@@ -1,6 +1,8 @@
-"""Turn a profile_round.sh output dir into profiles/<tag>/ summaries + profiles/pmc_traffic.json.
+"""Turn a profile_round.sh output dir into profiles/<tag>/ summaries + an entry of
+profiles/pmc_traffic.json (one per profiled workload: topology, replicas, hops).
 
-HBM bytes per launch of prisma_step_kernel = 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
+HBM bytes per launch of the step kernel (prisma_step_kernel_t / prisma_mem_step_kernel)
+= 2 * FETCH_SIZE * 1024 + WRITE_SIZE * 1024
 (MI355X_MICROARCH.md 'HBM': FETCH_SIZE counts half the bytes of wide coalesced reads on
 gfx950 — our staging reads are 16 B/lane; WRITE_SIZE is exact for 16-B stores, our
 record stores are 4-8 B and are reported as measured, uncalibrated).
@@ -14,7 +16,7 @@ os.makedirs(dst, exist_ok=True)
 
 
 def vals(path, counter):
-    rows = [r for r in csv.DictReader(open(path)) if "prisma_step_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    rows = [r for r in csv.DictReader(open(path)) if "step_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
     return [float(r["Counter_Value"]) for r in rows]
 
 
@@ -32,7 +34,15 @@ out = {
     "correction": "read x2 (gfx950 FETCH_SIZE half-count for 16-B/lane streaming reads); writes as measured",
     "dispatches": len(fetch), "tag": tag,
 }
-json.dump(out, open(os.path.join(root, "profiles", "pmc_traffic.json"), "w"), indent=1)
+path = os.path.join(root, "profiles", "pmc_traffic.json")
+try:
+    old = json.load(open(path))
+    entries = old.get("entries", [old] if "kernel" in old else [])
+except (OSError, ValueError):
+    entries = []
+key = lambda e: (e["topology"], e["replicas"], e["hops"])
+entries = [e for e in entries if key(e) != key(out)] + [out]
+json.dump({"entries": entries}, open(path, "w"), indent=1)
 shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
 shutil.copy(os.path.join(src, "pmc_fetch", "run_counter_collection.csv"), os.path.join(dst, "pmc_fetch_size.csv"))
 shutil.copy(os.path.join(src, "pmc_write", "run_counter_collection.csv"), os.path.join(dst, "pmc_write_size.csv"))

@@ -4,7 +4,7 @@ tot = collections.defaultdict(list)
 for p in ["a", "b", "c"]:
     try:
         for r in csv.DictReader(open(f"{d}/{p}/run_counter_collection.csv")):
-            if "prisma_step" in r["Kernel_Name"]:
+            if "step_kernel" in r["Kernel_Name"]:
                 tot[r["Counter_Name"]].append(float(r["Counter_Value"]))
     except FileNotFoundError:
         pass
