@@ -81,6 +81,10 @@ __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t lane) {
 __device__ __forceinline__ uint32_t wrl(uint32_t old, uint32_t v, uint32_t lane) {
     return threadIdx.x == lane ? v : old;
 }
+// lane `src` of v (a wave-wide ds_bpermute; src < 64, no lane-id arithmetic as in __shfl)
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src) {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src << 2), (int)v);
+}
 __device__ __forceinline__ int64_t mk64(uint32_t lo, uint32_t hi) { return (int64_t)(((uint64_t)hi << 32) | lo); }
 __device__ __forceinline__ uint32_t lo32(int64_t v) { return (uint32_t)(uint64_t)v; }
 __device__ __forceinline__ uint32_t hi32(int64_t v) { return (uint32_t)((uint64_t)v >> 32); }
@@ -631,7 +635,7 @@ __device__ __forceinline__ uint32_t observe_links(const Sim& S, const Regs<FS, L
                                   H.ping_rounds, now_s);
         else
             val = R.qb.v[j];
-        const uint32_t g = (uint32_t)__shfl((int)val, (int)(src & 63u));
+        const uint32_t g = bperm(val, src & 63u);
         if ((src >> 6) == (uint32_t)j) o = g;
     }
     return (lane >= 1 && lane <= deg) ? o : 0u;
@@ -656,7 +660,7 @@ __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_
     case 6: hw = node | (dst << 8) | (start << 16); break;
     default: hw = w7; break;
     }
-    uint32_t ob = (uint32_t)__shfl((int)obs_reg, (lane - 8) & 63);
+    uint32_t ob = bperm(obs_reg, (uint32_t)(lane - 8) & 63u);
     uint32_t word = lane < 8 ? hw : ob;
     uint32_t* p = (uint32_t*)(S.logrep + (size_t)(d & (S.lv.log_cap() - 1)) * S.lv.rec_bytes());
     if (lane < 8 + S.lv.W()) p[lane] = word;
