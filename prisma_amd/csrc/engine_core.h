@@ -45,7 +45,7 @@ static __device__ unsigned int g_prisma_trace_cap;
 static __device__ unsigned int g_prisma_trace_n[8];
 #endif
 #if PRISMA_TIMING
-static __device__ unsigned long long g_prisma_timing[16];   // one copy per engine (translation unit)
+static __device__ unsigned long long g_prisma_timing[32];   // one copy per engine (translation unit); 16-19: mlp_action phases
 #define TM_NOW() ((uint64_t)__builtin_amdgcn_s_memtime())
 #endif
 
@@ -64,6 +64,7 @@ struct KParams {
     int32_t* node_out;           // [R] or null
     const uint8_t* table;        // [N][N] or null
     const float* mlp;            // packed DQN-buffer weights or null (mode 4)
+    const float* mlp_rp;         // layers 2-4 of `mlp` interleaved by 4 inputs (mlp_repack), mode 4
     int32_t R;
     int32_t max_hops;
     uint32_t episode;            // reset kernel only
@@ -270,6 +271,7 @@ struct Sim {
     const CAS TopoImage* T;                 // topology (scalar loads at fixed offsets)
     const uint8_t* table;
     const float* mlp;                       // DQN-buffer weights (HBM) or null
+    const float* mlp_rp;                    // layers 2-4 interleaved by 4 inputs (mlp_repack)
     float* hbuf;                            // 64 floats of LDS: a layer's activations
     unsigned char* logrep;
     uint32_t gid;
@@ -288,6 +290,7 @@ struct Sim {
     uint32_t* lrec;                         // link records [L][kLRec] (HBM)
 #if PRISMA_TIMING
     mutable uint64_t tsub[2], tlast;             // sub-phase cycles inside apply_decision
+    mutable uint64_t tmlp[4];                    // mlp_action phases (timing build)
 #endif
 };
 
@@ -307,6 +310,7 @@ __device__ inline void sim_bind(Sim& S, const LV& L, unsigned char* lds, const u
     S.table = (const uint8_t*)(lds + L.lds_state_bytes());
     S.hbuf = (float*)(lds + L.s_mlp());
     S.mlp = nullptr;
+    S.mlp_rp = nullptr;
     S.logrep = logrep;
     S.gid = gid;
     S.lane = lane;
@@ -851,13 +855,41 @@ __device__ __forceinline__ void on_flow(const Sim& S, RS& R, Hot& H, uint32_t f)
 // DESIGN.md §2, restated by the oracle's mlp_action): lane j computes unit j of
 // each layer, activations are broadcast through 64 floats of LDS, weights are
 // read per lane from HBM (L2-resident, shared by every replica).
-__device__ __forceinline__ float hb_ld(const Sim& S, int i) { return S.hbuf[i]; }
+// Layers 2-4 read their weights from the interleaved copy (mlp_repack, filled by
+// prisma_run from the caller's row-major weights): for each node and layer, chunk c holds
+// W[4c..4c+3][j] as one float4 per output unit j, followed by the bias row. Lane j then
+// loads 16 coalesced 16-B values per layer instead of 64 dependent 4-B ones, and the
+// accumulation order (input 0, 1, ..., 63, one fmaf each) is unchanged.
+__host__ __device__ constexpr int mlp_rp_layer_floats(int units) { return 64 * units + units; }
+__host__ __device__ constexpr int mlp_rp_node_floats(int D) {   // rounded to whole float4s
+    return (2 * mlp_rp_layer_floats(64) + mlp_rp_layer_floats(D) + 3) & ~3;
+}
 
-__device__ __forceinline__ float mlp_dense64(const Sim& S, const float* __restrict__ W, int lane, int stride) {
+#ifndef PRISMA_MLP_BATCH
+#define PRISMA_MLP_BATCH 4
+#endif
+__device__ __forceinline__ float mlp_dense64(const Sim& S, const float* __restrict__ Wl, int lane, int units) {
+    constexpr int B = PRISMA_MLP_BATCH;                 // float4 loads in flight per lane
+    const float4* __restrict__ W4 = (const float4*)Wl;
+    const float4* __restrict__ hb = (const float4*)S.hbuf;
+    const float b = Wl[64 * units + lane];
     float acc = 0.0f;
-#pragma unroll 16
-    for (int i = 0; i < 64; ++i) acc = __builtin_fmaf(hb_ld(S, i), W[i * stride + lane], acc);
-    return acc;
+#pragma unroll
+    for (int c0 = 0; c0 < 16; c0 += B) {
+        float4 w[B];
+#pragma unroll
+        for (int c = 0; c < B; ++c) w[c] = W4[(c0 + c) * units + lane];
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+            const float4 h = hb[c0 + c];
+            acc = __builtin_fmaf(h.x, w[c].x, acc);
+            acc = __builtin_fmaf(h.y, w[c].y, acc);
+            acc = __builtin_fmaf(h.z, w[c].z, acc);
+            acc = __builtin_fmaf(h.w, w[c].w, acc);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return __fadd_rn(acc, b);
 }
 
 // one-hot input: obs[0] (the destination's overlay index, lane 0 of obs_reg)
@@ -869,12 +901,13 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     const float* __restrict__ b1 = W1 + N * N * 32;
     const float* __restrict__ Wb = b1 + N * 32;
     const float* __restrict__ bb = Wb + N * D * 32;
-    const float* __restrict__ W2 = bb + N * 32;
-    const float* __restrict__ b2 = W2 + N * 64 * 64;
-    const float* __restrict__ W3 = b2 + N * 64;
-    const float* __restrict__ b3 = W3 + N * 64 * 64;
-    const float* __restrict__ W4 = b3 + N * 64;
-    const float* __restrict__ b4 = W4 + N * 64 * D;
+    const float* __restrict__ RP = S.mlp_rp + (size_t)v * mlp_rp_node_floats(D);
+#if PRISMA_TIMING
+    uint64_t tq = TM_NOW(), tq1;
+#define TM_MLP(i) do { tq1 = TM_NOW(); S.tmlp[i] += tq1 - tq; tq = tq1; } while (0)
+#else
+#define TM_MLP(i) do { } while (0)
+#endif
     const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
     const uint32_t dst = rdl(obs_reg, 0);
     // LayerNormalization of the deg buffer values (population variance, epsilon 1e-3)
@@ -903,16 +936,19 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     }
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
-    h = det_elu(__fadd_rn(mlp_dense64(S, W2 + (int)v * 64 * 64, lane, 64), b2[(int)v * 64 + lane]));
+    TM_MLP(0);
+    h = det_elu(mlp_dense64(S, RP, lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
-    h = det_elu(__fadd_rn(mlp_dense64(S, W3 + (int)v * 64 * 64, lane, 64), b3[(int)v * 64 + lane]));
+    TM_MLP(1);
+    h = det_elu(mlp_dense64(S, RP + mlp_rp_layer_floats(64), lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
+    TM_MLP(2);
     float q = 0.0f;
-    if (lane < deg) q = det_elu(__fadd_rn(mlp_dense64(S, W4 + (int)v * 64 * D, lane, D), b4[(int)v * D + lane]));
+    if (lane < deg) q = det_elu(mlp_dense64(S, RP + 2 * mlp_rp_layer_floats(64), lane, D));
     __builtin_amdgcn_wave_barrier();
     // tf.argmin: first minimum (learner.py:145)
     int best = 0;
@@ -921,6 +957,7 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
         const float qa = __uint_as_float(rdl(__float_as_uint(q), (uint32_t)a));
         if (qa < bq) { bq = qa; best = a; }
     }
+    TM_MLP(3);
     return best;
 }
 
@@ -1402,6 +1439,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
     const bool mlp_mode = MLP;
     const bool table_mode = (P.mode == 2) || mlp_mode;            // fused in-kernel policy
     S.mlp = P.mlp;
+    S.mlp_rp = P.mlp_rp;
     const uint32_t max_hops = (uint32_t)P.max_hops;
     const uint32_t NN = (uint32_t)L.N();
     Hot H;
@@ -1433,6 +1471,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
     uint32_t tm_cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t tm_a = 0, tm_b = 0;
     S.tsub[0] = 0; S.tsub[1] = 0; S.tlast = 0;
+    S.tmlp[0] = 0; S.tmlp[1] = 0; S.tmlp[2] = 0; S.tmlp[3] = 0;
 #define TM_MARK(i) do { tm_b = TM_NOW(); tm_acc[i] += tm_b - tm_a; tm_cnt[i]++; tm_a = tm_b; } while (0)
 #else
 #define TM_MARK(i) do { } while (0)
@@ -1508,6 +1547,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
             atomicAdd(&g_prisma_timing[i], (unsigned long long)tm_acc[i]);
             atomicAdd(&g_prisma_timing[8 + i], (unsigned long long)tm_cnt[i]);
         }
+        for (int i = 0; i < 4; ++i) atomicAdd(&g_prisma_timing[16 + i], (unsigned long long)S.tmlp[i]);
     }
 #endif
 

@@ -26,6 +26,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <new>
 #include <string>
 #include <vector>
@@ -144,6 +145,43 @@ extern "C" __global__ void __launch_bounds__(256) prisma_gather_kernel(
     }
 }
 
+// DQN-buffer layers 2-4, row-major [in][out] in the caller's packed weights
+// (StackedQNet.pack(), models.py:258-306), copied into the interleaved per-node blocks
+// mlp_dense64 reads: rp[v][layer][c][j][q] = W[4c+q][j], then the layer's bias row.
+__global__ void prisma_mlp_repack_kernel(const float* __restrict__ w, float* __restrict__ rp, int N, int D) {
+    const int node_f = mlp_rp_node_floats(D);
+    const size_t n = (size_t)N * node_f;
+    const float* W2 = w + (size_t)N * N * 32 + (size_t)N * 32 + (size_t)N * D * 32 + (size_t)N * 32;
+    const float* b2 = W2 + (size_t)N * 64 * 64;
+    const float* W3 = b2 + (size_t)N * 64;
+    const float* b3 = W3 + (size_t)N * 64 * 64;
+    const float* W4 = b3 + (size_t)N * 64;
+    const float* b4 = W4 + (size_t)N * 64 * D;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const int v = (int)(i / node_f);
+        int o = (int)(i - (size_t)v * node_f);
+        const float *Wl, *bl;
+        int units;
+        if (o < mlp_rp_layer_floats(64)) {
+            Wl = W2 + (size_t)v * 64 * 64; bl = b2 + (size_t)v * 64; units = 64;
+        } else if (o < 2 * mlp_rp_layer_floats(64)) {
+            o -= mlp_rp_layer_floats(64);
+            Wl = W3 + (size_t)v * 64 * 64; bl = b3 + (size_t)v * 64; units = 64;
+        } else {
+            o -= 2 * mlp_rp_layer_floats(64);
+            Wl = W4 + (size_t)v * 64 * D; bl = b4 + (size_t)v * D; units = D;
+        }
+        float x = 0.0f;                                   // alignment padding
+        if (o < 64 * units) {
+            const int c = o / (4 * units), r = o - c * 4 * units, j = r >> 2, q = r & 3;
+            x = Wl[(4 * c + q) * units + j];
+        } else if (o < mlp_rp_layer_floats(units)) {
+            x = bl[o - 64 * units];
+        }
+        rp[i] = x;
+    }
+}
+
 // ===========================================================================
 // host side: sizing, validation, C-ABI
 // ===========================================================================
@@ -159,6 +197,7 @@ struct prisma_env {
     const void* k_step = nullptr;
     const void* k_step_mlp = nullptr;
     const void* k_reset = nullptr;
+    float* d_mlp_rp = nullptr;           // interleaved DQN-buffer layers 2-4 (prisma_run, mode 4)
     bool reset_done = false;
 };
 
@@ -171,8 +210,8 @@ extern "C" int prisma_abi_version(void) { return PRISMA_ABI_VERSION; }
 // diagnostic build only: read and clear the per-phase cycle totals
 extern "C" int prisma_debug_timing(unsigned long long* out16) {
     if (!HIP_OK(hipDeviceSynchronize()) ||
-        !HIP_OK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prisma_timing), 16 * sizeof(unsigned long long)))) return -1;
-    unsigned long long z[16] = {0};
+        !HIP_OK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prisma_timing), 32 * sizeof(unsigned long long)))) return -1;
+    unsigned long long z[32] = {0};
     return HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_timing), z, sizeof(z))) ? 0 : -1;
 }
 #endif
@@ -726,6 +765,18 @@ extern "C" int prisma_run(prisma_env_t* e, int32_t policy, const void* policy_da
     } else {
         P.mode = 4;
         P.mlp = (const float*)policy_data;
+        // the weights may change between calls (training): re-interleave them every call,
+        // on the caller's stream ahead of the step kernel (~1 us at GEANT size)
+        const int N = e->lay.N, D = e->lay.max_deg;
+        const size_t n = (size_t)N * mlp_rp_node_floats(D);
+        (void)hipSetDevice(e->device);
+        if (!e->d_mlp_rp && !HIP_OK(hipMalloc(&e->d_mlp_rp, n * sizeof(float))))
+            return set_err(PRISMA_ERR_NOMEM, "hipMalloc of the interleaved DQN-buffer weights failed");
+        const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 4096);
+        hipLaunchKernelGGL(prisma_mlp_repack_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream,
+                           P.mlp, e->d_mlp_rp, N, D);
+        if (!HIP_OK(hipGetLastError())) return set_err(PRISMA_ERR_LAUNCH, "repack kernel launch failed");
+        P.mlp_rp = e->d_mlp_rp;
     }
     P.max_hops = max_hops;
     int rc = launch(e, P.mode == 4 ? e->k_step_mlp : e->k_step, P, stream);
@@ -826,5 +877,6 @@ extern "C" void prisma_destroy(prisma_env_t* e) {
     if (e->d_log) (void)hipFree(e->d_log);
     if (e->d_cnt) (void)hipFree(e->d_cnt);
     if (e->d_lay) (void)hipFree(e->d_lay);
+    if (e->d_mlp_rp) (void)hipFree(e->d_mlp_rp);
     delete e;
 }

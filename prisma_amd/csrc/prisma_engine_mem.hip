@@ -395,6 +395,7 @@ __global__ void __launch_bounds__(64) prisma_mem_step_kernel(KParams P) {
     MemSt R;
     mem_bind(S, R, P, lv, lds, r, lane);
     S.mlp = P.mlp;
+    S.mlp_rp = P.mlp_rp;
     event_loop<MLP>(P, S, R, r);
     mem_stage(lds, P, r, lane, true);
 }
@@ -420,8 +421,8 @@ extern "C" int prisma_debug_trace(void* dev_buf, unsigned int cap) {
 // diagnostic build only: read and clear the memory-resident engine's per-phase cycle totals
 extern "C" int prisma_debug_timing_mem(unsigned long long* out16) {
     if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prisma_timing), 16 * sizeof(unsigned long long)) != hipSuccess) return -1;
-    unsigned long long z[16] = {0};
+        hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prisma_timing), 32 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    unsigned long long z[32] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -36,18 +36,23 @@ from prisma_amd.topology import Topology  # noqa: E402
 topo_name = sys.argv[sys.argv.index("--topology") + 1] if "--topology" in sys.argv else "abilene"
 R = int(sys.argv[sys.argv.index("--replicas") + 1]) if "--replicas" in sys.argv else 4096
 HOPS = int(sys.argv[sys.argv.index("--hops") + 1]) if "--hops" in sys.argv else 2048
+POLICY = sys.argv[sys.argv.index("--policy") + 1] if "--policy" in sys.argv else "dq_routing"
+PAO = int(sys.argv[sys.argv.index("--ping-as-obs") + 1]) if "--ping-as-obs" in sys.argv else 1
 topo = Topology.example(topo_name)
-eng = PrismaEngine(topo, engine_params(topo, sim_time_s=60.0, ping_as_obs=1, auto_reset=1,
+eng = PrismaEngine(topo, engine_params(topo, sim_time_s=60.0, ping_as_obs=PAO, auto_reset=1,
                                       log_capacity=65536 if topo.n_links > 256 else 8192), R)
 lib = load_library()
 timing = lib.prisma_debug_timing_mem if eng.engine_kind == 2 else lib.prisma_debug_timing
 timing.argtypes = [C.c_void_p]
-table = StackedQNet(topo, "routing", seed=1234).argmin_table()
+if POLICY == "dqn_buffer":
+    table = StackedQNet(topo, "buffer", seed=1234, device="cuda").pack()
+else:
+    table = StackedQNet(topo, "routing", seed=1234, device="cuda").argmin_table()
 eng.reset(0)
 WARM = int(sys.argv[sys.argv.index("--warm") + 1]) if "--warm" in sys.argv else 1
 for _ in range(WARM):
     eng.run(table, HOPS)
-buf = (C.c_ulonglong * 16)()
+buf = (C.c_ulonglong * 32)()
 timing(buf)
 h0 = int(eng.counters()["hops_total"].sum())
 for _ in range(4):
@@ -55,8 +60,12 @@ for _ in range(4):
 timing(buf)
 hops = int(eng.counters()["hops_total"].sum()) - h0
 tot = sum(buf[i] for i in range(8))
-print(f"{topo_name} R={R}: cycles/hop/wave = {tot / max(1, hops):.0f}")
+print(f"{topo_name} {POLICY} pao={PAO} R={R}: cycles/hop/wave = {tot / max(1, hops):.0f}")
 for i in range(8):
     n = buf[8 + i] if i < 6 else buf[8 + 2]
     if n and buf[i]:
         print(f"  {NAMES[i]:11s} n/hop={n / hops:.3f}  cyc/call={buf[i] / n:8.0f}  share={buf[i] / tot:.3f}")
+if buf[16]:
+    nd = buf[8 + 2]
+    for i, nm in enumerate(["mlp:ln+l1", "mlp:l2", "mlp:l3", "mlp:l4+argmin"]):
+        print(f"  {nm:13s} cyc/decision={buf[16 + i] / max(1, nd):8.0f}")
