@@ -855,14 +855,19 @@ __device__ __forceinline__ void on_flow(const Sim& S, RS& R, Hot& H, uint32_t f)
 // DESIGN.md §2, restated by the oracle's mlp_action): lane j computes unit j of
 // each layer, activations are broadcast through 64 floats of LDS, weights are
 // read per lane from HBM (L2-resident, shared by every replica).
-// Layers 2-4 read their weights from the interleaved copy (mlp_repack, filled by
-// prisma_run from the caller's row-major weights): for each node and layer, chunk c holds
-// W[4c..4c+3][j] as one float4 per output unit j, followed by the bias row. Lane j then
-// loads 16 coalesced 16-B values per layer instead of 64 dependent 4-B ones, and the
-// accumulation order (input 0, 1, ..., 63, one fmaf each) is unchanged.
+// The layers read their weights from an interleaved per-node copy (prisma_mlp_repack_kernel,
+// filled by prisma_run from the caller's row-major weights). Node block = [L1][L2][L3][L4]:
+// * L1: the buffers branch, chunk c holding Wb[4c..4c+3][j] as one float4 per unit j < 32
+//   (rows k >= D zero), then bb[32] and b1[32] (the one-hot rows of W1 stay in the caller's
+//   buffer: one row per decision);
+// * L2, L3, L4: chunk c holding W[4c..4c+3][j] as one float4 per output unit j, then the
+//   bias row.
+// Lane j loads one coalesced 16-B value per 4 inputs instead of 4 dependent 4-B ones, and
+// the accumulation order (input 0, 1, 2, ..., one fmaf each) is unchanged.
+__host__ __device__ constexpr int mlp_rp_l1_floats(int D) { return 128 * ((D + 3) / 4) + 64; }
 __host__ __device__ constexpr int mlp_rp_layer_floats(int units) { return 64 * units + units; }
 __host__ __device__ constexpr int mlp_rp_node_floats(int D) {   // rounded to whole float4s
-    return (2 * mlp_rp_layer_floats(64) + mlp_rp_layer_floats(D) + 3) & ~3;
+    return (mlp_rp_l1_floats(D) + 2 * mlp_rp_layer_floats(64) + mlp_rp_layer_floats(D) + 3) & ~3;
 }
 
 #ifndef PRISMA_MLP_BATCH
@@ -893,15 +898,15 @@ __device__ __forceinline__ float mlp_dense64(const Sim& S, const float* __restri
 }
 
 // one-hot input: obs[0] (the destination's overlay index, lane 0 of obs_reg)
+__device__ __forceinline__ float rdlf(float x, uint32_t k) { return __uint_as_float(rdl(__float_as_uint(x), k)); }
+
 __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs_reg) {
     const LV& L = S.lv;
     const int lane = S.lane;
     const int N = L.N(), D = L.max_deg();
     const float* __restrict__ W1 = S.mlp;
-    const float* __restrict__ b1 = W1 + N * N * 32;
-    const float* __restrict__ Wb = b1 + N * 32;
-    const float* __restrict__ bb = Wb + N * D * 32;
-    const float* __restrict__ RP = S.mlp_rp + (size_t)v * mlp_rp_node_floats(D);
+    const float* __restrict__ RP1 = S.mlp_rp + (size_t)v * mlp_rp_node_floats(D);
+    const float* __restrict__ RP = RP1 + mlp_rp_l1_floats(D);
 #if PRISMA_TIMING
     uint64_t tq = TM_NOW(), tq1;
 #define TM_MLP(i) do { tq1 = TM_NOW(); S.tmlp[i] += tq1 - tq; tq = tq1; } while (0)
@@ -910,30 +915,48 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
 #endif
     const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
     const uint32_t dst = rdl(obs_reg, 0);
-    // LayerNormalization of the deg buffer values (population variance, epsilon 1e-3)
+    // layer-1 weights first (independent of the normalisation): one W1 row element and
+    // b1 for the one-hot branch (lanes 0-31), the Wb chunks and bb for the buffers branch
+    // (lanes 32-63; deg <= D, so at most ceil(D/4) chunks)
+    const int j32 = lane & 31;
+    const int nck = (deg + 3) >> 2;
+    const float4* __restrict__ Wb4 = (const float4*)RP1;
+    const float b1v = (lane < 32) ? RP1[128 * ((D + 3) / 4) + 32 + j32] : RP1[128 * ((D + 3) / 4) + j32];
+    const float w1v = (lane < 32) ? W1[((int)v * N + (int)dst) * 32 + j32] : 0.0f;
+    float4 wb[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) wb[c] = (c < nck) ? Wb4[c * 32 + j32] : make_float4(0.f, 0.f, 0.f, 0.f);
+    // LayerNormalization of the deg buffer values (population variance, epsilon 1e-3):
+    // lane k+1 holds buffer value k; sums run in k order through readlanes
+    const float xf = (float)obs_reg;
     float sum = 0.0f;
-    for (int k = 0; k < deg; ++k) sum = __fadd_rn(sum, (float)rdl(obs_reg, (uint32_t)(k + 1)));
+    for (int k = 0; k < deg; ++k) sum = __fadd_rn(sum, rdlf(xf, (uint32_t)(k + 1)));
     const float mean = __fdiv_rn(sum, (float)deg);
+    const float dv = __fsub_rn(xf, mean);
+    const float sq = __fmul_rn(dv, dv);
     float var = 0.0f;
-    for (int k = 0; k < deg; ++k) {
-        const float d = __fsub_rn((float)rdl(obs_reg, (uint32_t)(k + 1)), mean);
-        var = __fadd_rn(var, __fmul_rn(d, d));
-    }
+    for (int k = 0; k < deg; ++k) var = __fadd_rn(var, rdlf(sq, (uint32_t)(k + 1)));
     var = __fdiv_rn(var, (float)deg);
     const float den = __fsqrt_rn(__fadd_rn(var, 1e-3f));
-    // layer 1: one-hot(dst) branch in lanes 0-31, buffers branch in lanes 32-63
-    float h;
-    if (lane < 32) {
-        h = det_elu(__fadd_rn(W1[((int)v * N + (int)dst) * 32 + lane], b1[(int)v * 32 + lane]));
-    } else {
-        const int j = lane - 32;
-        float acc = 0.0f;
-        for (int k = 0; k < deg; ++k) {
-            const float xn = __fdiv_rn(__fsub_rn((float)rdl(obs_reg, (uint32_t)(k + 1)), mean), den);
-            acc = __builtin_fmaf(xn, Wb[((int)v * D + k) * 32 + j], acc);
+    const float xn = __fdiv_rn(dv, den);                          // lane k+1: normalised value k
+    // layer 1: one-hot(dst) branch in lanes 0-31, buffers branch in lanes 32-63. The
+    // buffers dot product runs with every lane active (lanes 0-31 discard it): its
+    // readlanes read xn from lanes 1..deg, which must not sit in an inactive branch.
+    float acc = 0.0f;
+    for (int c = 0; c < nck; ++c) {
+        float4 w;
+        if (c < 4) {
+            w = (c == 0) ? wb[0] : (c == 1) ? wb[1] : (c == 2) ? wb[2] : wb[3];
+        } else {
+            w = Wb4[c * 32 + j32];
         }
-        h = det_elu(__fadd_rn(acc, bb[(int)v * 32 + j]));
+        const int k = 4 * c;
+        acc = __builtin_fmaf(rdlf(xn, (uint32_t)(k + 1)), w.x, acc);
+        if (k + 1 < deg) acc = __builtin_fmaf(rdlf(xn, (uint32_t)(k + 2)), w.y, acc);
+        if (k + 2 < deg) acc = __builtin_fmaf(rdlf(xn, (uint32_t)(k + 3)), w.z, acc);
+        if (k + 3 < deg) acc = __builtin_fmaf(rdlf(xn, (uint32_t)(k + 4)), w.w, acc);
     }
+    float h = det_elu(__fadd_rn(lane < 32 ? w1v : acc, b1v));
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
     TM_MLP(0);

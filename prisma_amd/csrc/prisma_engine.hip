@@ -145,13 +145,17 @@ extern "C" __global__ void __launch_bounds__(256) prisma_gather_kernel(
     }
 }
 
-// DQN-buffer layers 2-4, row-major [in][out] in the caller's packed weights
-// (StackedQNet.pack(), models.py:258-306), copied into the interleaved per-node blocks
-// mlp_dense64 reads: rp[v][layer][c][j][q] = W[4c+q][j], then the layer's bias row.
+// DQN-buffer weights, row-major [in][out] in the caller's packed buffer (StackedQNet.pack(),
+// models.py:258-306), copied into the interleaved per-node blocks mlp_action reads
+// (engine_core.h, mlp_rp_*): rp[v] = [Wb chunks, bb, b1][W2 chunks, b2][W3 chunks, b3][W4 chunks, b4].
 __global__ void prisma_mlp_repack_kernel(const float* __restrict__ w, float* __restrict__ rp, int N, int D) {
     const int node_f = mlp_rp_node_floats(D);
+    const int l1_f = mlp_rp_l1_floats(D), kc = (D + 3) / 4;
     const size_t n = (size_t)N * node_f;
-    const float* W2 = w + (size_t)N * N * 32 + (size_t)N * 32 + (size_t)N * D * 32 + (size_t)N * 32;
+    const float* b1 = w + (size_t)N * N * 32;
+    const float* Wb = b1 + (size_t)N * 32;
+    const float* bb = Wb + (size_t)N * D * 32;
+    const float* W2 = bb + (size_t)N * 32;
     const float* b2 = W2 + (size_t)N * 64 * 64;
     const float* W3 = b2 + (size_t)N * 64;
     const float* b3 = W3 + (size_t)N * 64 * 64;
@@ -160,23 +164,35 @@ __global__ void prisma_mlp_repack_kernel(const float* __restrict__ w, float* __r
     for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
         const int v = (int)(i / node_f);
         int o = (int)(i - (size_t)v * node_f);
-        const float *Wl, *bl;
-        int units;
-        if (o < mlp_rp_layer_floats(64)) {
-            Wl = W2 + (size_t)v * 64 * 64; bl = b2 + (size_t)v * 64; units = 64;
-        } else if (o < 2 * mlp_rp_layer_floats(64)) {
-            o -= mlp_rp_layer_floats(64);
-            Wl = W3 + (size_t)v * 64 * 64; bl = b3 + (size_t)v * 64; units = 64;
+        float x = 0.0f;                                   // padding (rows k >= D, alignment)
+        if (o < l1_f) {
+            if (o < 128 * kc) {
+                const int c = o / 128, r = o - c * 128, j = r >> 2, q = r & 3, k = 4 * c + q;
+                if (k < D) x = Wb[((size_t)v * D + k) * 32 + j];
+            } else if (o < 128 * kc + 32) {
+                x = bb[(size_t)v * 32 + (o - 128 * kc)];
+            } else {
+                x = b1[(size_t)v * 32 + (o - 128 * kc - 32)];
+            }
         } else {
-            o -= 2 * mlp_rp_layer_floats(64);
-            Wl = W4 + (size_t)v * 64 * D; bl = b4 + (size_t)v * D; units = D;
-        }
-        float x = 0.0f;                                   // alignment padding
-        if (o < 64 * units) {
-            const int c = o / (4 * units), r = o - c * 4 * units, j = r >> 2, q = r & 3;
-            x = Wl[(4 * c + q) * units + j];
-        } else if (o < mlp_rp_layer_floats(units)) {
-            x = bl[o - 64 * units];
+            o -= l1_f;
+            const float *Wl, *bl;
+            int units;
+            if (o < mlp_rp_layer_floats(64)) {
+                Wl = W2 + (size_t)v * 64 * 64; bl = b2 + (size_t)v * 64; units = 64;
+            } else if (o < 2 * mlp_rp_layer_floats(64)) {
+                o -= mlp_rp_layer_floats(64);
+                Wl = W3 + (size_t)v * 64 * 64; bl = b3 + (size_t)v * 64; units = 64;
+            } else {
+                o -= 2 * mlp_rp_layer_floats(64);
+                Wl = W4 + (size_t)v * 64 * D; bl = b4 + (size_t)v * D; units = D;
+            }
+            if (o < 64 * units) {
+                const int c = o / (4 * units), r = o - c * 4 * units, j = r >> 2, q = r & 3;
+                x = Wl[(4 * c + q) * units + j];
+            } else if (o < mlp_rp_layer_floats(units)) {
+                x = bl[o - 64 * units];
+            }
         }
         rp[i] = x;
     }
