@@ -870,11 +870,10 @@ __host__ __device__ constexpr int mlp_rp_node_floats(int D) {   // rounded to wh
     return (mlp_rp_l1_floats(D) + 2 * mlp_rp_layer_floats(64) + mlp_rp_layer_floats(D) + 3) & ~3;
 }
 
-#ifndef PRISMA_MLP_BATCH
-#define PRISMA_MLP_BATCH 4
-#endif
+// B: float4 weight loads in flight per lane (one L2 round trip per B chunks); 4 where the
+// kernel must fit 128 VGPRs (4 waves per SIMD), more where it has 256
+template <int B>
 __device__ __forceinline__ float mlp_dense64(const Sim& S, const float* __restrict__ Wl, int lane, int units) {
-    constexpr int B = PRISMA_MLP_BATCH;                 // float4 loads in flight per lane
     const float4* __restrict__ W4 = (const float4*)Wl;
     const float4* __restrict__ hb = (const float4*)S.hbuf;
     const float b = Wl[64 * units + lane];
@@ -900,6 +899,7 @@ __device__ __forceinline__ float mlp_dense64(const Sim& S, const float* __restri
 // one-hot input: obs[0] (the destination's overlay index, lane 0 of obs_reg)
 __device__ __forceinline__ float rdlf(float x, uint32_t k) { return __uint_as_float(rdl(__float_as_uint(x), k)); }
 
+template <int B>
 __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs_reg) {
     const LV& L = S.lv;
     const int lane = S.lane;
@@ -960,18 +960,18 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
     TM_MLP(0);
-    h = det_elu(mlp_dense64(S, RP, lane, 64));
+    h = det_elu(mlp_dense64<B>(S, RP, lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
     TM_MLP(1);
-    h = det_elu(mlp_dense64(S, RP + mlp_rp_layer_floats(64), lane, 64));
+    h = det_elu(mlp_dense64<B>(S, RP + mlp_rp_layer_floats(64), lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
     TM_MLP(2);
     float q = 0.0f;
-    if (lane < deg) q = det_elu(mlp_dense64(S, RP + 2 * mlp_rp_layer_floats(64), lane, D));
+    if (lane < deg) q = det_elu(mlp_dense64<B>(S, RP + 2 * mlp_rp_layer_floats(64), lane, D));
     __builtin_amdgcn_wave_barrier();
     // tf.argmin: first minimum (learner.py:145)
     int best = 0;
@@ -1455,7 +1455,7 @@ __device__ __forceinline__ void publish_counters(const Sim& S, const KParams& P,
 // then one discrete event per iteration until max_hops hops, a decision that
 // needs an external action, or the end of the episode; publish the outputs.
 // ---------------------------------------------------------------------------
-template <bool MLP, class RS>
+template <bool MLP, int MB, class RS>
 __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int r) {
     const int lane = S.lane;
     const LV& L = S.lv;
@@ -1473,7 +1473,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
     if (H.pend && !H.over) {
         if (table_mode) {
             uint32_t pn = u_ld32(&S.h->pend_node), pd = u_ld32(&S.h->pend_ent[1]);
-            const int a = mlp_mode ? mlp_action(S, pn, (lane < L.W()) ? S.obs[lane] : 0u)
+            const int a = mlp_mode ? mlp_action<MB>(S, pn, (lane < L.W()) ? S.obs[lane] : 0u)
                                    : (int)rfl((uint32_t)S.table[pn * NN + pd]);
             H.hops_launch += finish_pending(S, R, H, a);
         } else if (P.actions) {
@@ -1531,7 +1531,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
             TM_MARK(1);
             if (need) {
                 if (table_mode) {
-                    const int a = mlp_mode ? mlp_action(S, D.v, D.obs)
+                    const int a = mlp_mode ? mlp_action<MB>(S, D.v, D.obs)
                                            : (int)rfl((uint32_t)S.table[D.v * NN + D.dst]);
                     apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, a, true,
                                    D.reward, D.prev, D.obs,

@@ -81,6 +81,10 @@ __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
 // once, 2 (<= 256) up to 512 flows x 128 links
 template <int FS, int LS> struct StepOcc {
     static constexpr int waves = (FS <= 2 && LS == 1) ? 4 : (LS <= 2 ? 2 : 1);
+#ifndef PRISMA_MLP_B_WIDE
+#define PRISMA_MLP_B_WIDE 8
+#endif
+    static constexpr int mlp_batch = waves >= 4 ? 4 : PRISMA_MLP_B_WIDE;   // DQN-buffer loads in flight
 };
 
 // MLP: the in-kernel DQN-buffer policy is compiled in (mode 4 only); the table /
@@ -99,7 +103,7 @@ prisma_step_kernel_t(KParams P) {
     Sim S;
     sim_bind(S, lv, lds, P.topo, P.log + (size_t)r * LC.log_cap * LC.rec_bytes, LC.replica_base + (uint32_t)r, lane);
     S.tun = TUN;
-    event_loop<MLP>(P, S, R, r);
+    event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P, S, R, r);
     stage_out(lds, P, r, lane, R);
 }
 

@@ -396,7 +396,10 @@ __global__ void __launch_bounds__(64) prisma_mem_step_kernel(KParams P) {
     mem_bind(S, R, P, lv, lds, r, lane);
     S.mlp = P.mlp;
     S.mlp_rp = P.mlp_rp;
-    event_loop<MLP>(P, S, R, r);
+#ifndef PRISMA_MLP_B_MEM
+#define PRISMA_MLP_B_MEM 16
+#endif
+    event_loop<MLP, PRISMA_MLP_B_MEM>(P, S, R, r);
     mem_stage(lds, P, r, lane, true);
 }
 
