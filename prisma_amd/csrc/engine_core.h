@@ -269,7 +269,9 @@ struct Sim {
     float* win;
     float* pbd;                             // ping-back delays [responder slot][PBK]
     const CAS TopoImage* T;                 // topology (scalar loads at fixed offsets)
-    const uint8_t* table;
+    const uint8_t* table;                   // action table in LDS (register engine, table_in_lds)
+    const uint8_t* table_g;                 // ... or in HBM (memory-resident engine, or not in LDS)
+    bool tab_lds;
     const float* mlp;                       // DQN-buffer weights (HBM) or null
     const float* mlp_rp;                    // layers 2-4 interleaved by 4 inputs (mlp_repack)
     float* hbuf;                            // 64 floats of LDS: a layer's activations
@@ -308,6 +310,8 @@ __device__ inline void sim_bind(Sim& S, const LV& L, unsigned char* lds, const u
     S.pbd = (float*)(lds + L.s_pbd());
     S.T = (const CAS TopoImage*)topo;
     S.table = (const uint8_t*)(lds + L.lds_state_bytes());
+    S.table_g = nullptr;
+    S.tab_lds = true;
     S.hbuf = (float*)(lds + L.s_mlp());
     S.mlp = nullptr;
     S.mlp_rp = nullptr;
@@ -1413,10 +1417,14 @@ __device__ __forceinline__ void select_event(const Sim& S, const Regs<FS, LS>& R
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
-// the [N][N] action table (table policy) sits in LDS after the state image
+// the [N][N] action table (table policy) sits in LDS after the state image, or in HBM
+__device__ __forceinline__ int table_action(const Sim& S, uint32_t i) {
+    return (int)rfl(S.tab_lds ? (uint32_t)S.table[i] : (uint32_t)S.table_g[i]);
+}
+
 __device__ __forceinline__ void stage_table(unsigned char* lds, const KParams& P, int lane) {
     CLayout& LC = *(CLayout*)P.lay;
-    if (P.table) {
+    if (P.table && LC.table_in_lds) {
         uint8_t* dstp = lds + LC.lds_state_bytes;
         const uint32_t nt = (uint32_t)(LC.N * LC.N);
         for (uint32_t i = (uint32_t)lane; i < nt; i += kWave) dstp[i] = P.table[i];
@@ -1463,6 +1471,8 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
     const bool table_mode = (P.mode == 2) || mlp_mode;            // fused in-kernel policy
     S.mlp = P.mlp;
     S.mlp_rp = P.mlp_rp;
+    S.table_g = P.table;
+    S.tab_lds = S.tab_lds && ((CLayout*)P.lay)->table_in_lds != 0u;
     const uint32_t max_hops = (uint32_t)P.max_hops;
     const uint32_t NN = (uint32_t)L.N();
     Hot H;
@@ -1474,7 +1484,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
         if (table_mode) {
             uint32_t pn = u_ld32(&S.h->pend_node), pd = u_ld32(&S.h->pend_ent[1]);
             const int a = mlp_mode ? mlp_action<MB>(S, pn, (lane < L.W()) ? S.obs[lane] : 0u)
-                                   : (int)rfl((uint32_t)S.table[pn * NN + pd]);
+                                   : table_action(S, pn * NN + pd);
             H.hops_launch += finish_pending(S, R, H, a);
         } else if (P.actions) {
             finish_pending(S, R, H, (int)rfl((uint32_t)P.actions[r]));
@@ -1532,7 +1542,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
             if (need) {
                 if (table_mode) {
                     const int a = mlp_mode ? mlp_action<MB>(S, D.v, D.obs)
-                                           : (int)rfl((uint32_t)S.table[D.v * NN + D.dst]);
+                                           : table_action(S, D.v * NN + D.dst);
                     apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, a, true,
                                    D.reward, D.prev, D.obs,
                                    (D.flags & PEND_ECHO) ? (uint32_t)t_lrev(S, id) : kNoLink, D.last, D.ttl);

@@ -156,6 +156,10 @@ struct Layout {
     uint32_t s_lkey, s_lkind;    // LDS offsets of the link leaf keys (time lo, seq) and kinds (bytes)
     // topology image offsets (memory-resident engine; variable-size arrays)
     uint32_t t_rowptr, t_ldst, t_lrev, t_acctx, t_fsrc, t_fdst, t_fmean;
+    // register-resident engine: the [N][N] action table is staged into LDS (after the state
+    // image) only where that costs no replica per CU; otherwise it is read from HBM (L2)
+    uint32_t table_in_lds;
+    uint32_t lds_mlp_bytes;      // LDS of a DQN-buffer launch (its 256 B of activations included)
 };
 constexpr uint32_t kLVWords = 64u;           // Layout dwords held in the LV register
 

@@ -436,7 +436,9 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
     L.FS = L.LS = 0;
     L.ring_total = ring_total;
     L.lds_bytes = L.lds_state_bytes;                // the action table stays in HBM
+    L.table_in_lds = 0;
     L.s_mlp = L.lds_bytes;
+    L.lds_mlp_bytes = L.lds_bytes + 256u;
     if (L.lds_bytes + 256u > 160u * 1024u)
         return set_err(PRISMA_ERR_CONFIG, "event tree exceeds the 160 KiB LDS of a gfx950 CU");
     return PRISMA_OK;
@@ -655,9 +657,19 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.lds_state_bytes = o;
     L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 19u * 64u * (uint32_t)ls));
     L.state_bytes = o;
-    L.lds_bytes = L.lds_state_bytes + align16(L.table_bytes);
-    L.s_mlp = L.lds_bytes;                          // + 256 B of DQN-buffer activations (MLP launches only)
-    if (L.lds_bytes + 256u > 160u * 1024u)
+    // Replicas per CU are bounded by LDS (160 KiB / bytes per replica) for the larger
+    // topologies, and a launch whose replicas do not all fit at once runs in rounds
+    // (GEANT + MLP: 2 048 replicas at 7 per CU took two rounds, the second 1/8 full).
+    // So the action table goes to LDS only where it costs no replica per CU (else the
+    // decision reads it from HBM, L2-resident), and the DQN-buffer activations reuse the
+    // table's LDS, dead in MLP launches, when it is there.
+    const uint32_t tb = align16(L.table_bytes);
+    auto per_cu = [](uint32_t b) { return (160u * 1024u) / (b ? b : 1u); };
+    L.table_in_lds = per_cu(L.lds_state_bytes + tb) == per_cu(L.lds_state_bytes) ? 1u : 0u;
+    L.lds_bytes = L.lds_state_bytes + (L.table_in_lds ? tb : 0u);
+    L.s_mlp = (L.table_in_lds && tb >= 256u) ? L.lds_state_bytes : L.lds_bytes;
+    L.lds_mlp_bytes = L.s_mlp + 256u > L.lds_bytes ? L.s_mlp + 256u : L.lds_bytes;
+    if (L.lds_mlp_bytes > 160u * 1024u)
         return set_err(PRISMA_ERR_CONFIG, "replica state exceeds the 160 KiB LDS of a gfx950 CU");
 
     return PRISMA_OK;
@@ -709,7 +721,7 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
         e->k_reset = pick_kernel(L.FS, L.LS, 1, false);
         e->k_step_mlp = pick_kernel(L.FS, L.LS, 2, L.tunnels != 0u);
     }
-    (void)hipFuncSetAttribute(e->k_step_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes + 256);
+    (void)hipFuncSetAttribute(e->k_step_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_mlp_bytes);
     (void)hipFuncSetAttribute(e->k_step, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
     (void)hipFuncSetAttribute(e->k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
     *out = e;
@@ -731,7 +743,7 @@ static KParams base_params(prisma_env_t* e) {
 static int launch(prisma_env_t* e, const void* kern, KParams P, void* stream) {
     (void)hipSetDevice(e->device);
     void* args[] = { &P };
-    const size_t lds = e->lay.lds_bytes + (kern == e->k_step_mlp ? 256u : 0u);
+    const size_t lds = kern == e->k_step_mlp ? e->lay.lds_mlp_bytes : e->lay.lds_bytes;
     hipError_t err = hipLaunchKernel(kern, dim3((unsigned)e->R), dim3(kWave), args, lds, (hipStream_t)stream);
     if (err == hipSuccess) err = hipGetLastError();
     if (err != hipSuccess) return set_err(PRISMA_ERR_LAUNCH, std::string("kernel launch failed: ") + hipGetErrorString(err));

@@ -269,6 +269,8 @@ __device__ __forceinline__ void mem_bind(Sim& S, MemSt& R, const KParams& P, con
     S.pbd = (float*)(img + LC.s_pbd);
     S.lrec = (uint32_t*)(img + LC.g_lrec);
     S.table = P.table;
+    S.table_g = P.table;
+    S.tab_lds = false;
     const CAS unsigned char* tb = (const CAS unsigned char*)P.topo;
     S.m_rowptr = (const CAS int32_t*)(tb + LC.t_rowptr);
     S.m_ldst = (const CAS int32_t*)(tb + LC.t_ldst);
