@@ -900,6 +900,43 @@ __device__ __forceinline__ float mlp_dense64(const Sim& S, const float* __restri
     return __fadd_rn(acc, b);
 }
 
+// B == kMlpAll (memory-resident engine, one wave per SIMD and VGPRs to spare): every
+// weight of layers 2-4 is loaded when the decision starts, one round trip in all
+constexpr int kMlpAll = 64;
+struct MlpPre {
+    float4 w2[16], w3[16], w4[16];
+    float b2, b3, b4;
+};
+
+__device__ __forceinline__ void mlp_preload(MlpPre& M, const float* __restrict__ RP, int lane, int D, int deg) {
+    const float4* __restrict__ W2 = (const float4*)RP;
+    const float4* __restrict__ W3 = (const float4*)(RP + mlp_rp_layer_floats(64));
+    const float4* __restrict__ W4 = (const float4*)(RP + 2 * mlp_rp_layer_floats(64));
+#pragma unroll
+    for (int c = 0; c < 16; ++c) M.w2[c] = W2[c * 64 + lane];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) M.w3[c] = W3[c * 64 + lane];
+#pragma unroll
+    for (int c = 0; c < 16; ++c) M.w4[c] = lane < deg ? W4[c * D + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    M.b2 = RP[64 * 64 + lane];
+    M.b3 = RP[mlp_rp_layer_floats(64) + 64 * 64 + lane];
+    M.b4 = lane < deg ? RP[2 * mlp_rp_layer_floats(64) + 64 * D + lane] : 0.0f;
+}
+
+__device__ __forceinline__ float mlp_dense64_pre(const Sim& S, const float4 (&w)[16], float b) {
+    const float4* __restrict__ hb = (const float4*)S.hbuf;
+    float acc = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+        const float4 h = hb[c];
+        acc = __builtin_fmaf(h.x, w[c].x, acc);
+        acc = __builtin_fmaf(h.y, w[c].y, acc);
+        acc = __builtin_fmaf(h.z, w[c].z, acc);
+        acc = __builtin_fmaf(h.w, w[c].w, acc);
+    }
+    return __fadd_rn(acc, b);
+}
+
 // one-hot input: obs[0] (the destination's overlay index, lane 0 of obs_reg)
 __device__ __forceinline__ float rdlf(float x, uint32_t k) { return __uint_as_float(rdl(__float_as_uint(x), k)); }
 
@@ -919,6 +956,8 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
 #endif
     const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
     const uint32_t dst = rdl(obs_reg, 0);
+    MlpPre M;
+    if constexpr (B == kMlpAll) mlp_preload(M, RP, lane, D, deg);
     // layer-1 weights first (independent of the normalisation): one W1 row element and
     // b1 for the one-hot branch (lanes 0-31), the Wb chunks and bb for the buffers branch
     // (lanes 32-63; deg <= D, so at most ceil(D/4) chunks)
@@ -964,18 +1003,25 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
     TM_MLP(0);
-    h = det_elu(mlp_dense64<B>(S, RP, lane, 64));
+    if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w2, M.b2));
+    else h = det_elu(mlp_dense64<B>(S, RP, lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
     TM_MLP(1);
-    h = det_elu(mlp_dense64<B>(S, RP + mlp_rp_layer_floats(64), lane, 64));
+    if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w3, M.b3));
+    else h = det_elu(mlp_dense64<B>(S, RP + mlp_rp_layer_floats(64), lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
     TM_MLP(2);
     float q = 0.0f;
-    if (lane < deg) q = det_elu(mlp_dense64<B>(S, RP + 2 * mlp_rp_layer_floats(64), lane, D));
+    if constexpr (B == kMlpAll) {
+        const float q4 = det_elu(mlp_dense64_pre(S, M.w4, M.b4));
+        if (lane < deg) q = q4;
+    } else {
+        if (lane < deg) q = det_elu(mlp_dense64<B>(S, RP + 2 * mlp_rp_layer_floats(64), lane, D));
+    }
     __builtin_amdgcn_wave_barrier();
     // tf.argmin: first minimum (learner.py:145)
     int best = 0;

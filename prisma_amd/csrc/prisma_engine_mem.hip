@@ -399,7 +399,7 @@ __global__ void __launch_bounds__(64) prisma_mem_step_kernel(KParams P) {
     S.mlp = P.mlp;
     S.mlp_rp = P.mlp_rp;
 #ifndef PRISMA_MLP_B_MEM
-#define PRISMA_MLP_B_MEM 16
+#define PRISMA_MLP_B_MEM kMlpAll
 #endif
     event_loop<MLP, PRISMA_MLP_B_MEM>(P, S, R, r);
     mem_stage(lds, P, r, lane, true);
