@@ -62,6 +62,8 @@ def lib():
         L.or_mlp_action.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
         L.or_det_expm1.restype = C.c_double
         L.or_det_expm1.argtypes = [C.c_double]
+        L.or_det_expm1f.restype = C.c_float
+        L.or_det_expm1f.argtypes = [C.c_float]
         L.or_pending_node.restype = C.c_int32
         L.or_pending_node.argtypes = [C.c_void_p]
         L.or_record_count.restype = C.c_int64
@@ -91,6 +93,11 @@ def lib():
 
 def det_expm1(x: float) -> float:
     return float(lib().or_det_expm1(float(x)))
+
+
+def det_expm1f(x: float) -> float:
+    """The fp32 expm1 of the DQN-buffer ELU (x <= 0), as the engine computes it."""
+    return float(lib().or_det_expm1f(float(x)))
 
 
 def philox(ctr, key):

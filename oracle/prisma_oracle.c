@@ -891,7 +891,28 @@ double or_det_expm1(double x) {                 /* x <= 0; + - * / only */
     return scale * (p + 1.0) - 1.0;
 }
 
-static float elu_f(float x) { return x > 0.0f ? x : (float)or_det_expm1((double)x); }
+/* fp32 expm1 for x <= 0, + - * and an int conversion only: the engine's det_expm1f
+ * (prisma_amd/csrc/numerics.h), the same operations in the same order. */
+float or_det_expm1f(float x) {
+    if (!(x == x)) return x;
+    if (x < -17.0f) return -1.0f;
+    if (x > -5.9604645e-08f) return x;
+    const float t = x * 1.44269504f + 0.5f;
+    int ki = (int)t;
+    if ((float)ki > t) ki -= 1;
+    const float k = (float)ki;
+    const float r = (x - k * 0.693145751953125f) - k * 1.42860677e-06f;
+    static const float c[6] = { 1.38888889e-03f, 8.33333333e-03f, 4.16666667e-02f, 1.66666667e-01f, 0.5f, 1.0f };
+    float p = r * 1.98412698e-04f;
+    for (int i = 0; i < 6; ++i) p = (p + c[i]) * r;
+    if (ki == 0) return p;
+    uint32_t bits = (uint32_t)(127 + ki) << 23;
+    float scale;
+    memcpy(&scale, &bits, 4);
+    return scale * (p + 1.0f) - 1.0f;
+}
+
+static float elu_f(float x) { return x > 0.0f ? x : or_det_expm1f(x); }
 
 /* Packed weights (float): W1[N][N][32] b1[N][32] Wb[N][D][32] bb[N][32] W2[N][64][64] b2[N][64]
  * W3[N][64][64] b3[N][64] W4[N][64][D] b4[N][D], D = max_deg (prisma_amd.policies.StackedQNet.pack). */

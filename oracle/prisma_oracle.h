@@ -77,6 +77,7 @@ int or_step(or_sim_t* s, int32_t action, int32_t* obs_out);
 int64_t or_run_mlp(or_sim_t* s, const float* weights, int64_t max_hops);
 int32_t or_mlp_action(or_sim_t* s, const float* weights, int32_t v, const uint32_t* obs);
 double or_det_expm1(double x);
+float or_det_expm1f(float x);
 
 /* Node of the pending notification (-1 if none). */
 int32_t or_pending_node(const or_sim_t* s);

@@ -272,6 +272,24 @@ def test_det_expm1_accuracy(oracle_mod):
         assert abs(got - want) <= 4e-16 * max(1.0, abs(want)) + 1e-300, (x, got, want)
 
 
+def test_det_expm1f_accuracy(oracle_mod):
+    """The MLP's fp32 ELU: within 2 ulp (fp32) of expm1 on (-inf, 0], exact at the edges."""
+    import math
+    rng = np.random.default_rng(0)
+    xs = [0.0, -0.0, -1e-30, -1e-8, -6e-8, -1e-6, -0.01, -0.3465, -0.3466, -0.5, -1.0, -2.0, -7.3, -16.99,
+          -17.0, -17.01, -20.0, -80.0]
+    xs += list(-rng.exponential(1.0, 20000)) + list(-rng.uniform(0, 1e-3, 2000))
+    worst = 0.0
+    for x in xs:
+        x = float(np.float32(x))
+        got, want = oracle_mod.det_expm1f(x), math.expm1(x)
+        ulp = float(np.spacing(np.float32(abs(want)))) if want != 0.0 else 1e-45
+        worst = max(worst, abs(got - want) / ulp)
+        assert abs(got - want) <= 2.0 * ulp, (x, got, want)
+    assert oracle_mod.det_expm1f(-100.0) == -1.0 and oracle_mod.det_expm1f(0.0) == 0.0
+    assert worst > 0.0
+
+
 def test_oracle_mlp_matches_torch_dqn_buffer(oracle_mod):
     """The oracle's fixed-order fp32 DQN_buffer_model picks torch's argmin (models.py:258-306)
     except on near-ties (different summation order)."""
