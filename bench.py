@@ -43,7 +43,8 @@ def parse():
                         "flow-start events are a transient of the episode)")
     p.add_argument("--replicas", type=int, default=None, help="replicas per GPU (default 4096; er256: 1024 = "
                                                              "BASELINE config 5's 8192 over 8 GPUs)")
-    p.add_argument("--hops", type=int, default=None, help="hops per replica per step (default 2048; er256: 8192)")
+    p.add_argument("--hops", type=int, default=8192, help="hops per replica per step (default 8192: one launch "
+                   "of ~60 ms at the headline, so the per-step policy refresh and launch costs stay ~1 %%)")
     p.add_argument("--topology", default="abilene")
     p.add_argument("--tm", type=int, default=0)
     p.add_argument("--load-factor", type=float, default=1.0)
@@ -56,8 +57,6 @@ def parse():
     big = a.topology == "er256"
     if a.replicas is None:
         a.replicas = 1024 if big else 4096
-    if a.hops is None:
-        a.hops = 8192 if big else 2048
     if a.warmup is None:
         a.warmup = 13 if big else 2          # er256: 13 x 8192 hops ~ 1.3 simulated seconds
     return a

@@ -9,10 +9,10 @@ OUT=gpurun_out/configs.jsonl
 B="timeout -k 10 300 python bench.py --cpu-baseline 0 --steps 5 --warmup 1"
 echo "config 1: abilene SP, 1 replica" && $B --policy sp --replicas 1 --hops 2048 >> $OUT
 echo "config 2: abilene DQ-routing, 4096" && $B >> $OUT
-echo "config 3: abilene on geant, DQN-buffer pingAsObs=1, 4096" && $B --topology abilene_on_geant --policy dqn_buffer --hops 1024 >> $OUT
+echo "config 3: abilene on geant, DQN-buffer pingAsObs=1, 4096" && $B --topology abilene_on_geant --policy dqn_buffer >> $OUT
 echo "config 3 (SP table)" && $B --topology abilene_on_geant --policy sp >> $OUT
 for lf in 0.5 0.75 1.0 1.25 1.5 1.75 2.0; do
-  echo "config 4: geant DQN-buffer pingAsObs=0 lf $lf, 2048" && $B --topology geant --policy dqn_buffer --ping-as-obs 0 --load-factor $lf --replicas 2048 --hops 1024 >> $OUT
+  echo "config 4: geant DQN-buffer pingAsObs=0 lf $lf, 2048" && $B --topology geant --policy dqn_buffer --ping-as-obs 0 --load-factor $lf --replicas 2048 >> $OUT
 done
 # ER-256: bench.py's defaults (1 024 replicas, 8 192 hops/step, 13 warmup steps past the
 # first simulated second's flow-start transient)
