@@ -265,6 +265,38 @@ def test_vec_env_transitions_match_oracle_join(oracle_mod):
     env.close()
 
 
+@pytest.mark.parametrize("name", ["geant", "er256"])
+def test_dqn_buffer_weights_change_between_launches(oracle_mod, name):
+    """prisma_run re-interleaves the caller's weights on every DQN-buffer launch (training
+    updates them in place): launches with weights A, then B written into the same tensor,
+    decide like the oracle run with A then B."""
+    from prisma_amd.policies import StackedQNet
+    topo = Topology.example(name)
+    wa = StackedQNet(topo, "buffer", seed=5).pack()
+    wb = StackedQNet(topo, "buffer", seed=6).pack()
+    params = engine_params(topo, sim_time_s=10.0, ping_as_obs=1, replica_base=1,
+                           log_capacity=65536 if topo.n_links > 256 else 8192)
+    R, H = 2, 600
+    eng = PrismaEngine(topo, params, R)
+    eng.reset(0)
+    w = wa.clone()
+    eng.run(w, H)
+    w.copy_(wb)                              # same pointer, new contents
+    eng.run(w, H)
+    torch.cuda.synchronize()
+    cnt = eng.counters()
+    log = eng.log_tensor().cpu().numpy()
+    for r in range(R):
+        o = oracle_mod.OracleSim(topo, params, replica=1 + r)
+        o.run_mlp(wa.cpu().numpy(), H)
+        o.run_mlp(wb.cpu().numpy(), H)
+        ref = o.records()
+        assert cnt[r]["error"] == 0
+        assert int(cnt[r]["dec_count"]) == len(ref)
+        assert eng.records(r, 0, len(ref), log_host=log).tobytes() == ref.tobytes(), r
+    eng.close()
+
+
 @pytest.mark.parametrize("name,ping,train", [("abilene", 1, 0), ("abilene", 0, 1), ("geant", 1, 0)])
 def test_dqn_buffer_in_kernel_parity(oracle_mod, name, ping, train):
     """PRISMA_POLICY_DQN_BUFFER: the in-kernel DQN_buffer_model decides exactly like the
