@@ -30,6 +30,11 @@ struct MemSt {
     uint4* lv1;                  // LDS [n1] {t lo, t hi, seq, code}
     uint4* lv2;                  // LDS [n2]
     uint32_t L, n_leaf, n1, n2, RW, WCAP;
+    // the 64-leaf block of the flow whose send event runs, loaded (one coalesced 1 KiB
+    // load) by flow_draw for its draw index; flow_set re-reduces the block from it instead
+    // of storing the new key and loading the block back (one HBM round trip per flow event)
+    uint4 fblk;
+    uint32_t fblk_b;             // its block index, or ~0u
 };
 
 constexpr int64_t kInf = INT64_MAX;
@@ -105,6 +110,31 @@ __device__ __forceinline__ Key group_min(const Sim& S, const MemSt& R, uint32_t 
     return wave_min_key(t, s, c);
 }
 
+// block_min of the cached flow block, with `leaf` holding the new key (t, seq, code); link
+// leaves of the block (the one straddling links and flows) are read from LDS as usual
+__device__ __forceinline__ Key block_min_cached(const Sim& S, const MemSt& R, uint32_t b, int64_t now, uint32_t leaf,
+                                                int64_t nt, uint32_t ns, uint32_t ncode) {
+    const uint32_t li = b * 64u + (uint32_t)S.lane;
+    int64_t t = kInf;
+    uint32_t s = 0xffffffffu, c = 0u;
+    if (li < R.L) {
+        const uint2 k = R.lkey[li];
+        const uint32_t kind = R.lkind[li];
+        if (kind) {
+            t = now + (int64_t)(uint32_t)(k.x - lo32(now));
+            s = k.y;
+        }
+        c = (kind << 28) | li;
+    } else if (li == leaf) {
+        t = nt; s = ns; c = ncode;
+    } else if (li < R.n_leaf) {
+        t = mk64(R.fblk.x, R.fblk.y);
+        s = R.fblk.z;
+        c = (K_FLOW << 28) | (li - R.L);
+    }
+    return wave_min_key(t, s, c);
+}
+
 // Source `leaf`'s next event changed to (t, seq): store its key and repair the two
 // tree levels above it.  A block is re-reduced only if the leaf was its minimum and
 // did not become smaller; a new smaller key just replaces it.
@@ -124,7 +154,7 @@ __device__ __forceinline__ void tree_touch(const Sim& S, MemSt& R, const Hot& H,
     if (key_less(t, seq, cur.t, cur.s)) {
         nb.t = t; nb.s = seq; nb.c = code;
     } else if (leaf_of(R, cur.c) == leaf) {
-        nb = block_min(S, R, b, H.now);
+        nb = (b == R.fblk_b) ? block_min_cached(S, R, b, H.now, leaf, t, seq, code) : block_min(S, R, b, H.now);
     } else {
         return;
     }
@@ -190,12 +220,16 @@ __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, u
 }
 
 // ---- flows ----
-__device__ __forceinline__ uint32_t flow_draw(const Sim& S, const MemSt& R, uint32_t f) {
-    return u_ld32(&R.fkeys[f].w);
+__device__ __forceinline__ uint32_t flow_draw(const Sim& S, MemSt& R, uint32_t f) {
+    const uint32_t leaf = R.L + f, b = leaf >> 6, li = b * 64u + (uint32_t)S.lane;
+    R.fblk = (li >= R.L && li < R.n_leaf) ? R.fkeys[li - R.L] : make_uint4(0u, 0u, 0u, 0u);
+    R.fblk_b = b;
+    return rdl(R.fblk.w, leaf & 63u);
 }
 __device__ __forceinline__ void flow_set(const Sim& S, MemSt& R, const Hot& H, uint32_t f, int64_t t, uint32_t seq,
                                          uint32_t draw) {
     tree_touch(S, R, H, R.L + f, t, seq, (K_FLOW << 28) | f, draw);
+    R.fblk_b = ~0u;
 }
 
 // ---- ping state of tunnel t (== link t: identity overlays only), words 8-15 ----
@@ -291,6 +325,8 @@ __device__ __forceinline__ void mem_bind(Sim& S, MemSt& R, const KParams& P, con
     R.n2 = LC.n2;
     R.RW = LC.lrec_words;
     R.WCAP = (uint32_t)LC.WCAP;
+    R.fblk = make_uint4(0u, 0u, 0u, 0u);
+    R.fblk_b = ~0u;
 }
 
 // episode start (sim.cc:610-630, data-packet-manager.cc:118-121): LDS header,
