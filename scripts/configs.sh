@@ -14,6 +14,7 @@ echo "config 3 (SP table)" && $B --topology abilene_on_geant --policy sp >> $OUT
 for lf in 0.5 0.75 1.0 1.25 1.5 1.75 2.0; do
   echo "config 4: geant DQN-buffer pingAsObs=0 lf $lf, 2048" && $B --topology geant --policy dqn_buffer --ping-as-obs 0 --load-factor $lf --replicas 2048 >> $OUT
 done
+echo "config 4 variant: geant DQN-buffer pingAsObs=1 lf 1.0, 2048" && $B --topology geant --policy dqn_buffer --ping-as-obs 1 --replicas 2048 >> $OUT
 # ER-256: bench.py's defaults (1 024 replicas, 8 192 hops/step, 13 warmup steps past the
 # first simulated second's flow-start transient)
 echo "config 5: ER-256 DQN-buffer pingAsObs=1, 1024" && $B --topology er256 --policy dqn_buffer --warmup 13 >> $OUT
