@@ -267,7 +267,11 @@ int prisma_step(prisma_env_t* env, const int32_t* actions, int32_t* obs_out,
 /* Fused policy: advance every replica by up to max_hops hops, deciding
  * in-kernel: PRISMA_POLICY_TABLE with `policy_data` = device uint8
  * [n_nodes][n_nodes] action table (SP, DQ-routing argmin), or
- * PRISMA_POLICY_DQN_BUFFER with `policy_data` = device packed fp32 weights.
+ * PRISMA_POLICY_DQN_BUFFER with `policy_data` = device packed fp32 weights
+ * (row-major, as StackedQNet.pack() lays them out; the library copies them
+ * into an interleaved per-node layout on `stream` before each such launch,
+ * so weights updated in place between calls take effect on the next call;
+ * calls on one env are ordered by their streams: keep one stream per env).
  * A replica stops early at the end of its episode; with params.auto_reset
  * it starts the next episode before the call returns (one launch never
  * crosses an episode boundary). */
