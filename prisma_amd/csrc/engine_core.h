@@ -463,7 +463,7 @@ __device__ __forceinline__ uint32_t flow_draw(const Sim& S, const Regs<FS, LS>& 
     return R.f_draw.get(f);
 }
 template <int FS, int LS>
-__device__ __forceinline__ void flow_min_refresh(const Sim& S, Regs<FS, LS>& R) {
+__device__ __forceinline__ void flow_min_refresh(const Sim& S, Regs<FS, LS>& R, const Hot& H) {
     int64_t ft = INT64_MAX;
     uint32_t s = 0xffffffffu, c = 0xffffffffu;
 #pragma unroll
@@ -472,6 +472,8 @@ __device__ __forceinline__ void flow_min_refresh(const Sim& S, Regs<FS, LS>& R) 
         const uint32_t sj = R.fk_seq.v[j];
         if (key_less(tj, sj, ft, s)) { ft = tj; s = sj; c = (K_FLOW << 28) | (uint32_t)(S.lane + 64 * j); }
     }
+    // the ping timer competes in lane 0 (refreshed when a round re-arms it)
+    if (S.lane == 0 && key_less(H.ping_t, H.ping_seq, ft, s)) { ft = H.ping_t; s = H.ping_seq; c = K_PING << 28; }
     R.fm_t = ft; R.fm_s = s; R.fm_c = c;
 }
 template <int FS, int LS>
@@ -481,7 +483,7 @@ __device__ __forceinline__ void flow_set(const Sim& S, Regs<FS, LS>& R, const Ho
     R.fk_hi.set(f, hi32(t));
     R.fk_seq.set(f, seq);
     R.f_draw.set(f, draw);
-    flow_min_refresh(S, R);
+    flow_min_refresh(S, R, H);
 }
 
 // ping state of tunnel t (ping_ack): oldest unacked round, acked mask, window
@@ -847,6 +849,7 @@ __device__ __forceinline__ void on_ping_round(const Sim& S, RS& R, Hot& H) {   /
     H.ev_launch += (uint32_t)(L.NO() - 1);
     H.ping_t = H.now + L.ping_period();
     H.ping_seq = first_rearm;
+    flow_min_refresh(S, R, H);
 }
 
 template <class RS>
@@ -1420,11 +1423,9 @@ __device__ __forceinline__ uint32_t sat_offset(int64_t t, int64_t now) {
 template <int FS, int LS>
 __device__ __forceinline__ void select_event(const Sim& S, const Regs<FS, LS>& R, const Hot& H, int lane, int64_t& bt,
                                              uint32_t& bc) {
-    // flows (each lane's cached earliest, flow_min_refresh) and the ping timer: exact
-    // 64-bit per-lane minimum, then one offset
+    // flows and the ping timer: each lane's cached earliest (flow_min_refresh), then one offset
     int64_t ft = R.fm_t;
     uint32_t s = R.fm_s, c = R.fm_c;
-    if (lane == 0 && key_less(H.ping_t, H.ping_seq, ft, s)) { ft = H.ping_t; s = H.ping_seq; c = K_PING << 28; }
     uint32_t k = sat_offset(ft, H.now);
     // links: 32-bit offsets
     const uint32_t n0 = lo32(H.now);
@@ -1535,7 +1536,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
     const uint32_t NN = (uint32_t)L.N();
     Hot H;
     hot_load(S, H);
-    flow_min_refresh(S, R);
+    flow_min_refresh(S, R, H);
 
     H.stop = 0;
     H.hops_launch = 0;

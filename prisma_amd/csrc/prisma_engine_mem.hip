@@ -220,7 +220,7 @@ __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, u
 }
 
 // ---- flows ----
-__device__ __forceinline__ void flow_min_refresh(const Sim&, MemSt&) {}   // the event tree keeps it
+__device__ __forceinline__ void flow_min_refresh(const Sim&, MemSt&, const Hot&) {}   // the event tree keeps it
 __device__ __forceinline__ uint32_t flow_draw(const Sim& S, MemSt& R, uint32_t f) {
     const uint32_t leaf = R.L + f, b = leaf >> 6, li = b * 64u + (uint32_t)S.lane;
     R.fblk = (li >= R.L && li < R.n_leaf) ? R.fkeys[li - R.L] : make_uint4(0u, 0u, 0u, 0u);
