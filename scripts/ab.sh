@@ -1,4 +1,5 @@
 #!/bin/bash
+# (_ab_old/ is listed in .gpurunignore to keep pushes small: remove that line before using this script; scripts/ab_lib.sh compares prebuilt libraries instead)
 # A/B throughput: _ab_old/ (a previous tree, built) vs the working tree, alternating, same box.
 ARGS="$*"
 for i in 1 2; do
