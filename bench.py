@@ -9,16 +9,22 @@ forward pass over every (node, dst)) + one engine launch in which every
 replica executes `--hops` forwarding decisions (enqueue or drop), logging
 one decision record per data notification to HBM.
 
-Run: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RCCL); replicas are sharded
-(weak scaling: replica ids rank*R .. rank*R+R-1), no data-path collective;
-the per-replica episode statistics are all-gathered over RCCL at the end.
+Run: python bench.py [--gpus N --steps K --warmup W].  N > 1: one process per
+GPU over RCCL, either under torch.distributed.run (RANK/WORLD_SIZE set) or
+launched by this script itself (it starts N child ranks before anything
+touches the GPU, then waits for them).  Replicas are sharded (weak scaling:
+replica ids rank*R .. rank*R+R-1), no data-path collective; the per-replica
+episode statistics are all-gathered over RCCL at the end.  --same-device runs
+the N ranks on cuda:0 over gloo (a rehearsal of the spawn/gather/JSON path on
+a one-GPU box; its value is not a scaling figure).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -29,8 +35,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "packet-hop transitions/sec at 4096 Abilene replicas; achieved HBM GB/s"   # BASELINE.json
-KERNEL_SOURCES = ["prisma_amd/csrc/prisma_engine.hip", "prisma_amd/csrc/prisma_engine_mem.hip",
-                  "prisma_amd/csrc/engine_core.h", "prisma_amd/csrc/engine_layout.h", "prisma_amd/csrc/numerics.h"]
 HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
@@ -53,6 +57,9 @@ def parse():
                    help="in-kernel policy: DQ-routing argmin table (BASELINE configs[1]), DQN-buffer MLP, SP table")
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-hops", type=int, default=8000000, help="oracle hops per host thread (cpu_baseline)")
+    p.add_argument("--cpu-hops-1core", type=int, default=4000000, help="oracle hops of the single-thread pass")
+    p.add_argument("--same-device", action="store_true",
+                   help="N ranks share cuda:0 over gloo (rehearsal of the N-rank path on one GPU)")
     a = p.parse_args()
     big = a.topology == "er256"
     if a.replicas is None:
@@ -67,83 +74,163 @@ def algorithmic_bytes(hops: int, deg_sum: int) -> int:
     return 85 * hops + 12 * deg_sum
 
 
-def cpu_baseline(topo, params, table, hops_per_thread: int):
-    """The C oracle (oracle/, kind 'port') on host threads: each thread runs one
-    replica's episodes back to back (as auto-reset does) until it executed
-    `hops_per_thread` hops, on the same scenario and DQ-routing table."""
+def host_cpus():
+    """(threads to use, description): the CPUs this process may actually run on — its affinity
+    set, capped by a cgroup CPU quota (on the GPU box `nproc` shows the whole machine, while the
+    job's quota is its share) — plus nproc and the CPU model name."""
+    nproc = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = nproc
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    use = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return use, {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "model": model}
+
+
+def cpu_baseline(topo, params, table, hops_per_thread: int, hops_1core: int):
+    """The C oracle (oracle/, kind 'port') on the host: one replica per thread over every CPU this
+    job may use (each thread runs back-to-back episodes, as auto-reset does, until it executed
+    `hops_per_thread` hops), and a single-thread pass for the per-core figure."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
-    cores = max(1, min(16, os.cpu_count() or 1))
-    done = [0] * cores
-    episodes = [0] * cores
+    cores, host = host_cpus()
 
-    def work(i):
-        ep = 0
-        while done[i] < hops_per_thread:
-            sim = O.OracleSim(topo, params, replica=100000 + i, episode=ep)
-            done[i] += sim.run_table(table, hops_per_thread - done[i])   # ctypes releases the GIL
-            sim.close()
-            ep += 1
-        episodes[i] = ep
+    def timed(n_threads, hops_each):
+        done = [0] * n_threads
+        episodes = [0] * n_threads
 
-    ths = [threading.Thread(target=work, args=(i,)) for i in range(cores)]
-    t0 = time.perf_counter()
-    for t in ths:
-        t.start()
-    for t in ths:
-        t.join()
-    dt = time.perf_counter() - t0
-    hops = int(sum(done))
-    return {"value": hops / dt, "unit": "hops/s", "cores": cores, "kind": "port",
-            "sample": f"{cores} host threads x {hops_per_thread} hops ({sum(episodes)} Abilene episodes of "
-                      f"{params['sim_time_s']:g} s, same params and DQ-routing table), {hops} hops in {dt:.1f} s wall; "
+        def work(i):
+            ep = 0
+            while done[i] < hops_each:
+                sim = O.OracleSim(topo, params, replica=100000 + i, episode=ep)
+                done[i] += sim.run_table(table, hops_each - done[i])   # ctypes releases the GIL
+                sim.close()
+                ep += 1
+            episodes[i] = ep
+
+        ths = [threading.Thread(target=work, args=(i,)) for i in range(n_threads)]
+        t0 = time.perf_counter()
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        dt = time.perf_counter() - t0
+        return int(sum(done)), int(sum(episodes)), dt
+
+    h1, e1, d1 = timed(1, hops_1core)
+    hn, en, dn = timed(cores, hops_per_thread)
+    return {"value": hn / dn, "unit": "hops/s", "cores": cores, "kind": "port",
+            "value_1core": h1 / d1, "host": host,
+            "sample": f"{cores} host threads x {hops_per_thread} hops ({en} Abilene episodes of "
+                      f"{params['sim_time_s']:g} s, same params and DQ-routing table), {hn} hops in {dn:.1f} s wall; "
+                      f"1 thread x {hops_1core} hops in {d1:.1f} s; {cores} = the CPUs this job may use "
+                      f"(affinity {host['affinity']}, cgroup quota {host['cgroup_quota_cpus']}, nproc {host['nproc']}); "
                       f"the ns-3 reference path is not runnable here (SURVEY 8c)"}
 
 
-def kernel_source_hash() -> str:
-    import hashlib
-    h = hashlib.sha1()
-    for f in KERNEL_SOURCES:
-        with open(os.path.join(ROOT, f), "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:12]
-
-
-def pmc_traffic(topology: str, replicas: int, hops: int):
-    """HBM bytes per launch from the committed rocprofv3 --pmc passes (profiles/pmc_traffic.json),
-    used only when they were collected on this workload with this exact kernel source."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def _profile_entry(name: str, topology: str, replicas: int, hops: int, build: str):
+    """The entry of a committed profile table (profiles/<name>.json) for this workload, used only
+    when it was collected with this exact library build (prisma_build_id())."""
     try:
-        with open(path) as fh:
+        with open(os.path.join(ROOT, "profiles", name)) as fh:
             d = json.load(fh)
-        for e in d.get("entries", [d]):
+        for e in d.get("entries", []):
             if (e.get("topology") == topology and int(e.get("replicas", -1)) == replicas
-                    and int(e.get("hops", -1)) == hops and e.get("kernel_source") == kernel_source_hash()):
-                return float(e["bytes_per_launch"])
+                    and int(e.get("hops", -1)) == hops and e.get("build_id") == build):
+                return e
     except (OSError, ValueError, KeyError):
         pass
     return None
 
 
+def pmc_traffic(topology: str, replicas: int, hops: int, build: str):
+    """HBM bytes per launch from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes."""
+    e = _profile_entry("pmc_traffic.json", topology, replicas, hops, build)
+    return None if e is None else float(e["bytes_per_launch"])
+
+
+def issue_roofline(topology: str, replicas: int, hops: int, build: str):
+    """Instruction-issue utilisation of the step kernel from the committed SQ counter passes
+    (profiles/pmc_sq.json, scripts/pmc_to_json.py): scalar-ALU instructions per CU-cycle (one
+    scalar unit per CU issues at most one per cycle) and wave64 VALU instructions per SIMD-cycle
+    (a SIMD-32 issues one every 2 cycles: peak 0.5), with the per-hop instruction counts."""
+    e = _profile_entry("pmc_sq.json", topology, replicas, hops, build)
+    if e is None:
+        return None
+    keys = ("salu_busy", "valu_busy", "salu_per_hop", "valu_per_hop", "branch_per_hop", "vmem_rd_per_hop",
+            "wait_mem_frac", "wait_dep_frac", "tag")
+    return {k: e[k] for k in keys if k in e}
+
+
+def launch_ranks(n: int) -> int:
+    """Start n child ranks of this script (one per GPU) and wait for them.  The parent touches no
+    GPU (no torch import at all) and does not exec: it runs the ranks as subprocesses with the
+    torch.distributed env contract and returns the worst exit status; a failing rank stops the rest."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0:
+                rc = rc or c
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    return rc
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
+    backend = "gloo" if args.same_device else "nccl"
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
     from prisma_amd.config import engine_params
     from prisma_amd.dist import gather_replica_stats, shard
-    from prisma_amd.engine import PrismaEngine
+    from prisma_amd.engine import PrismaEngine, build_id
     from prisma_amd.policies import StackedQNet
     from prisma_amd.topology import Topology, sp_next_hop_table
 
@@ -193,7 +280,7 @@ def main():
     t1 = time.perf_counter()
     elapsed = t1 - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     c1 = eng.counters()
@@ -201,26 +288,32 @@ def main():
     deg_avg = float(c1["hop_deg_sum"].sum()) / max(1, int(c1["hops"].sum()))   # mean deg(u) over hops
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     errors = int(c1["error"].max())
-    stats = gather_replica_stats(c1, world)                    # RCCL all-gather (outside the timed region)
-    hops_total = hops_local
+    stats = gather_replica_stats(c1, world, device=coll_dev)   # RCCL all-gather (outside the timed region)
+    per_rank = [hops_local]
     if world > 1:
-        ht = torch.tensor([hops_local], dtype=torch.int64, device=dev)
+        ht = torch.zeros(world, dtype=torch.int64, device=coll_dev)
+        ht[rank] = hops_local
         dist.all_reduce(ht)
-        hops_total = int(ht.item())
+        per_rank = [int(x) for x in ht.cpu().tolist()]
+        er = torch.tensor([errors], dtype=torch.int64, device=coll_dev)
+        dist.all_reduce(er, op=dist.ReduceOp.MAX)
+        errors = int(er.item())
+    hops_total = int(sum(per_rank))
 
     if rank == 0:
         # per-launch algorithmic bytes: the hops one launch executes on this rank x B_hop at their mean degree
         hops_per_launch = hops_local / args.steps
         alg_bytes = algorithmic_bytes(int(round(hops_per_launch)), int(round(hops_per_launch * deg_avg)))
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-        traffic = pmc_traffic(args.topology, args.replicas, args.hops)
+        bid = build_id()
+        traffic = pmc_traffic(args.topology, args.replicas, args.hops, bid)
         metric = METRIC if (args.topology, args.replicas) == ("abilene", 4096) else \
             f"packet-hop transitions/sec at {args.replicas} {topo.name} replicas; achieved HBM GB/s"
         result = {
             "metric": metric,
             "value": hops_total / elapsed,
             "unit": "hops/s",
-            "n_gpus": world,
+            "n_gpus": 1 if args.same_device else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": elapsed * 1e3 / args.steps,
@@ -235,21 +328,27 @@ def main():
                             f"{args.replicas} replicas/GPU x {args.hops} hops/step, pingAsObs={args.ping_as_obs}, "
                             f"simTime 60 s auto-reset",
                 "topology": args.topology, "replicas_per_gpu": args.replicas, "hops_per_step": args.hops,
-                "policy": args.policy, "parallelism": f"replica-sharded x{world}",
+                "policy": args.policy, "parallelism": f"replica-sharded x{world}"
+                + (" (ranks share cuda:0 over gloo: rehearsal, not a scaling figure)" if args.same_device else ""),
             },
             "roofline": {
                 "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": eng.kernel_name_mlp if args.policy == "dqn_buffer" else eng.kernel_name, "kernel_ms": kern_ms, "kernel_source": kernel_source_hash(),
+                "kernel": eng.kernel_name_mlp if args.policy == "dqn_buffer" else eng.kernel_name,
+                "kernel_ms": kern_ms, "build_id": bid,
                 "alg_bytes_per_launch": alg_bytes, "hops_per_launch": hops_per_launch,
+                # the binding resource: instruction issue (committed SQ counters of this build)
+                "issue": issue_roofline(args.topology, args.replicas, args.hops, bid),
             },
             "errors": errors,
             "episodes_completed": stats["episodes_completed"],
+            "replicas_total": int(stats["stats"].shape[0]),
+            "per_rank_hops_s": [h / elapsed for h in per_rank],
         }
         if args.cpu_baseline and world == 1 and args.policy != "dqn_buffer":
             result["cpu_baseline"] = cpu_baseline(topo, dict(params, auto_reset=0),
-                                                  policy().cpu().numpy(), args.cpu_hops)
+                                                  policy().cpu().numpy(), args.cpu_hops, args.cpu_hops_1core)
         print(json.dumps(result), flush=True)
     eng.close()
     if world > 1:

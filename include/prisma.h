@@ -242,6 +242,10 @@ typedef struct prisma_env prisma_env_t;
 
 int         prisma_abi_version(void);
 const char* prisma_last_error(void);
+/* 12 hex digits: hash of the sources + compile flags this library was built
+ * from (prisma_amd/buildid.py); loaders refuse a library whose id differs
+ * from the sources beside it. */
+const char* prisma_build_id(void);
 
 /* Size the per-replica state for this topology and allocate it on
  * `device`.  Validates shapes and ids up front. */

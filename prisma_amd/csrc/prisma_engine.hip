@@ -226,6 +226,14 @@ static int set_err(int code, const std::string& msg) { g_err = msg; return code;
 
 extern "C" int prisma_abi_version(void) { return PRISMA_ABI_VERSION; }
 
+// Source hash the library was built from (prisma_amd/buildid.py, passed by the build as
+// -DPRISMA_BUILD_ID); the marker lets the loader read it from the file without dlopen.
+#ifndef PRISMA_BUILD_ID
+#define PRISMA_BUILD_ID "unknown00000"
+#endif
+static const char k_build_id[] = "PRISMA_BUILD_ID=" PRISMA_BUILD_ID;
+extern "C" const char* prisma_build_id(void) { return k_build_id + 16; }
+
 #if PRISMA_TIMING
 // diagnostic build only: read and clear the per-phase cycle totals
 extern "C" int prisma_debug_timing(unsigned long long* out16) {

@@ -31,10 +31,13 @@ def replica_stats(counters: np.ndarray) -> np.ndarray:
 
 
 def gather_replica_stats(counters: np.ndarray, world: int, device=None) -> dict:
-    """All-gather every rank's per-replica statistics (equal R per rank) and summarise.
+    """All-gather every rank's per-replica statistics and summarise.
 
-    Returns {"stats": [world*R, F] ndarray in global replica order, "episodes_completed": int,
-    "mean_return": float, "delivered": int, "lost": int}.
+    Ranks may hold different replica counts (shard() of a total that world does not divide):
+    the counts are all-gathered first, every rank pads its block to the largest, and the
+    padding is cut out again, so the result is always [total, F] in global replica order.
+    Returns {"stats": [total, F] ndarray, "episodes_completed": int, "mean_return": float,
+    "delivered": int, "lost": int}.
     """
     import torch
     local = torch.from_numpy(replica_stats(counters))
@@ -43,10 +46,17 @@ def gather_replica_stats(counters: np.ndarray, world: int, device=None) -> dict:
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" \
                 else torch.device("cpu")
-        local = local.to(device)
-        out = torch.empty((world * local.shape[0], local.shape[1]), dtype=local.dtype, device=device)
-        dist.all_gather_into_tensor(out, local)
-        allst = out.cpu().numpy()
+        n = torch.tensor([local.shape[0]], dtype=torch.int64, device=device)
+        sizes = torch.empty(world, dtype=torch.int64, device=device)
+        dist.all_gather_into_tensor(sizes, n)
+        sizes = [int(x) for x in sizes.cpu().tolist()]
+        width = max(sizes)
+        block = torch.zeros((width, local.shape[1]), dtype=local.dtype, device=device)
+        block[:local.shape[0]] = local.to(device)
+        out = torch.empty((world * width, local.shape[1]), dtype=local.dtype, device=device)
+        dist.all_gather_into_tensor(out, block)
+        out = out.cpu().numpy()
+        allst = np.concatenate([out[r * width: r * width + sizes[r]] for r in range(world)])
     else:
         allst = local.numpy()
     ep = allst[:, STAT_FIELDS.index("episode")]

@@ -12,6 +12,7 @@ from typing import Optional
 
 import numpy as np
 
+from . import buildid
 from .records import COUNTERS_DTYPE, record_dtype
 from .topology import Topology
 
@@ -64,7 +65,7 @@ class _Plan(C.Structure):
 
 
 EXPORTS = [
-    "prisma_abi_version", "prisma_last_error", "prisma_create", "prisma_reset", "prisma_step", "prisma_run",
+    "prisma_abi_version", "prisma_last_error", "prisma_build_id", "prisma_create", "prisma_reset", "prisma_step", "prisma_run",
     "prisma_read_counters", "prisma_counters_device", "prisma_log_view", "prisma_copy_log",
     "prisma_copy_counters", "prisma_gather_records", "prisma_state_bytes", "prisma_plan", "prisma_destroy",
 ]
@@ -75,16 +76,25 @@ _lib = None
 def load_library(path: str = None):
     """Load libprisma_amd.so and declare its C-ABI (raises if absent).
 
-    PRISMA_LIB overrides the path (diagnostic builds, e.g. scripts/ablate.sh)."""
+    PRISMA_LIB overrides the path (diagnostic builds, e.g. scripts/ablate.sh).  The default
+    library must carry the build id of the sources beside it (prisma_amd/buildid.py): a stale
+    binary raises instead of running."""
     global _lib
     if _lib is not None:
         return _lib
-    path = path or os.environ.get("PRISMA_LIB") or LIB_PATH
+    override = path or os.environ.get("PRISMA_LIB")
+    path = override or LIB_PATH
     if not os.path.exists(path):
         raise PrismaError(f"{path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
     L = C.CDLL(path)
     L.prisma_abi_version.restype = C.c_int
     L.prisma_last_error.restype = C.c_char_p
+    L.prisma_build_id.restype = C.c_char_p
+    if not override and buildid.sources_present():
+        want, got = buildid.source_hash(), L.prisma_build_id().decode()
+        if got != want:
+            raise PrismaError(f"{path} was built from other sources (build id {got}, sources {want}): "
+                              f"rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
     L.prisma_create.restype = C.c_int
     L.prisma_create.argtypes = [C.POINTER(_Topo), C.POINTER(_Params), C.c_int32, C.c_int32, C.POINTER(C.c_void_p)]
     L.prisma_reset.restype = C.c_int
@@ -115,6 +125,11 @@ def load_library(path: str = None):
         raise PrismaError("libprisma_amd ABI version mismatch")
     _lib = L
     return L
+
+
+def build_id() -> str:
+    """Build id of the loaded library (prisma_build_id())."""
+    return load_library().prisma_build_id().decode()
 
 
 def _check(rc: int):

@@ -37,10 +37,10 @@ def _counters_for(base, n):
     return np.array(out)
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, total):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    base, n = shard(TOTAL + 1, rank, world)          # 6 replicas -> 3 per rank (equal shards)
+    base, n = shard(total, rank, world)
     res = gather_replica_stats(_counters_for(base, n), world, device=torch.device("cpu"))
     if rank == 0:
         q.put(res["stats"])
@@ -56,16 +56,17 @@ def test_shard_covers_all_replicas():
             assert ids == list(range(total))
 
 
-def test_gloo_world2_gather_equals_single_process(oracle_mod):
+@pytest.mark.parametrize("total", [TOTAL + 1, TOTAL])      # 3 + 3 (equal) and 3 + 2 (unequal shards)
+def test_gloo_world2_gather_equals_single_process(oracle_mod, total):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q, total)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    ref = replica_stats(_counters_for(0, TOTAL + 1))
+    ref = replica_stats(_counters_for(0, total))
     assert np.array_equal(got, ref)
