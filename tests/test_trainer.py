@@ -1,5 +1,8 @@
-"""Replay buffers and the Q-routing trainer (prisma_amd/trainer.py) against direct
-restatements of the reference's replay_buffer.py / learner.py / trainer.py math, on CPU."""
+"""Replay buffers and the Q-routing trainer (prisma_amd/trainer.py) against the
+reference's own ReplayBuffer (fixture) and restatements of learner.py / trainer.py math, on CPU."""
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -8,49 +11,42 @@ from prisma_amd.topology import Topology
 from prisma_amd.trainer import LinearSchedule, QRoutingTrainer, ReplayBuffers, huber
 
 
-class RefRing:
-    """replay_buffer.py:12-37 ReplayBuffer.add."""
-
-    def __init__(self, size):
-        self.storage, self.maxsize, self.next_idx, self.total = [], size, 0, 0
-
-    def add(self, item):
-        self.total += 1
-        if self.next_idx >= len(self.storage):
-            self.storage.append(item)
-        else:
-            self.storage[self.next_idx] = item
-        self.next_idx = (self.next_idx + 1) % self.maxsize
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "replay_buffer.json")
 
 
-def test_replay_buffers_match_per_node_rings():
-    rng = np.random.default_rng(0)
-    N, size, W = 5, 7, 4
+def _batch(bt, W):
+    return {"node": torch.tensor(bt["node"], dtype=torch.int64),
+            "obs": torch.tensor(bt["obs"], dtype=torch.int32).reshape(-1, W),
+            "next_obs": torch.tensor(bt["next_obs"], dtype=torch.int32).reshape(-1, W),
+            "action": torch.tensor(bt["action"], dtype=torch.int64),
+            "reward": torch.tensor(bt["reward"], dtype=torch.float64),
+            "done": torch.tensor(bt["done"], dtype=torch.bool)}
+
+
+def test_replay_buffers_match_reference_fixture():
+    """Per-node rings against the states the reference's own ReplayBuffer.add reached on the
+    same transition sequence (replay_buffer.py:12-37; tests/golden/make_replay_golden.py)."""
+    fx = json.load(open(GOLDEN))
+    N, size, W = fx["n_nodes"], fx["size"], fx["obs_width"]
     buf = ReplayBuffers(N, size, W, device="cpu")
-    refs = [RefRing(size) for _ in range(N)]
-    uid = 0
-    for batch in (3, 20, 1, 40, 0, 9):                     # includes batches that overflow a ring
-        node = rng.integers(0, N, batch)
-        obs = np.zeros((batch, W), dtype=np.int32)
-        obs[:, 0] = np.arange(uid, uid + batch)           # unique tag per transition
-        tr = {"node": torch.from_numpy(node), "obs": torch.from_numpy(obs),
-              "next_obs": torch.from_numpy(obs + 1), "action": torch.from_numpy(node % 3),
-              "reward": torch.from_numpy(rng.random(batch)), "done": torch.from_numpy(rng.random(batch) < 0.3)}
-        for i in range(batch):
-            refs[node[i]].add(int(obs[i, 0]))
-        uid += batch
-        buf.add(tr)
+    for bt, st in zip(fx["batches"], fx["states"]):
+        buf.add(_batch(bt, W))
         for u in range(N):
-            assert int(buf.count[u]) == len(refs[u].storage)
-            assert int(buf.total[u]) == refs[u].total
-            assert int(buf.next_idx[u]) == refs[u].next_idx
-            got = buf.obs[u, :len(refs[u].storage), 0].tolist()
-            assert got == refs[u].storage
-    o, a, r, no, d = buf.sample(16, torch.Generator().manual_seed(1))
+            assert int(buf.count[u]) == st[u]["len"]
+            assert int(buf.next_idx[u]) == st[u]["next_idx"]
+            assert int(buf.total[u]) == st[u]["total_samples"]
+            assert buf.obs[u, :st[u]["len"], 0].tolist() == st[u]["tags"]
+    for u in range(N):
+        for i, d in enumerate(fx["final"][u]):
+            assert buf.obs[u, i].tolist() == d["obs"]
+            assert buf.next_obs[u, i].tolist() == d["next_obs"]
+            assert int(buf.action[u, i]) == d["action"]
+            assert float(buf.reward[u, i]) == float(np.float32(d["reward"]))   # rings store f32 rewards
+            assert bool(buf.done[u, i]) == d["done"]
+    o, a, r, no, dn = buf.sample(16, torch.Generator().manual_seed(1))
     assert o.shape == (N, 16, W) and a.shape == (N, 16)
     for u in range(N):                                    # samples come from the node's own ring
-        assert set(o[u, :, 0].tolist()) <= set(refs[u].storage)
-        assert torch.equal(no[u], o[u] + 1)
+        assert set(o[u, :, 0].tolist()) <= set(fx["states"][-1][u]["tags"])
 
 
 def test_linear_schedule():
