@@ -269,7 +269,8 @@ struct Sim {
     prisma_counters_t* c;
     uint32_t* obs;
     uint32_t* wt; uint32_t* wseq;           // wire: arrival time (low 32 bits) and seq
-    uint32_t* ring;
+    uint32_t* went;                         // tunnelled overlays: wire packet entries (LDS)
+    uint32_t* ring;                         // link FIFOs: LDS, or HBM (tunnelled / memory-resident)
     float* win;
     float* pbd;                             // ping-back delays [responder slot][PBK]
     const CAS TopoImage* T;                 // topology (scalar loads at fixed offsets)
@@ -309,6 +310,7 @@ __device__ inline void sim_bind(Sim& S, const LV& L, unsigned char* lds, const u
     S.obs = (uint32_t*)(lds + kOffObs);
     S.wt = (uint32_t*)(lds + L.s_wt());
     S.wseq = (uint32_t*)(lds + L.s_wseq());
+    S.went = S.wseq + (uint32_t)L.L() * (uint32_t)L.WCAP();
     S.ring = (uint32_t*)(lds + L.s_ring());
     S.win = (float*)(lds + L.s_win());
     S.pbd = (float*)(lds + L.s_pbd());
@@ -344,6 +346,14 @@ __device__ __forceinline__ double t_fmean(const Sim& S, uint32_t f) { return S.m
 template <class T>
 __device__ __forceinline__ void st_rep(const Sim& S, T* p, T v) {
     if (S.mem || S.lane == 0) *p = v;
+}
+
+// A FIFO entry.  Identity overlays of the register-resident engine keep the rings in LDS
+// (lane 0 writes); tunnelled overlays and the memory-resident engine keep them in the HBM
+// state image, written by every lane like st_rep (their arrivals read the packet from
+// the wire slot, so only a dequeue behind a busy transmitter reads the ring back).
+__device__ __forceinline__ void ring_put(const Sim& S, uint32_t i, uint32_t e) {
+    if (S.mem || S.tun || S.lane == 0) S.ring[i] = e;
 }
 
 // uniform LDS reads (every lane reads the same address: broadcast, no conflict)
@@ -526,6 +536,7 @@ __device__ __forceinline__ void wire_set(const Sim& S, LinkV& k, uint32_t l, uin
     } else if (S.lane == 0) {
         S.wt[l * W + i] = t;
         S.wseq[l * W + i] = s;
+        if (S.tun) S.went[l * W + i] = x;
     }
 }
 __device__ __forceinline__ void wire_get(const Sim& S, const LinkV& k, uint32_t l, uint32_t i, uint32_t& t,
@@ -572,7 +583,7 @@ __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l
     if (!ok) return 0;
     uint32_t cap = ring_cap(S, l), off = ring_off(S, l);
     if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
-    st_rep(S, &S.ring[off + k.tail], e);
+    ring_put(S, off + k.tail, e);
     k.tail = (k.tail + 1 == cap) ? 0 : k.tail + 1;
     k.n_queue++;
     k.qb += size;
@@ -1148,8 +1159,10 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
     const LV& L = S.lv;
     const uint32_t v = (uint32_t)t_ldst(S, l);
     LinkV k = link_get(R, l);
-    const uint32_t x = S.mem ? wire_ent(S, k, k.head & (uint32_t)(L.WCAP() - 1))
-                             : u_ld32(&S.ring[ring_off(S, l) + k.head]);
+    const uint32_t wh = k.head & (uint32_t)(L.WCAP() - 1);
+    const uint32_t x = S.mem ? wire_ent(S, k, wh)
+                             : (S.tun ? u_ld32(&S.went[l * (uint32_t)L.WCAP() + wh])
+                                      : u_ld32(&S.ring[ring_off(S, l) + k.head]));
     const uint32_t type = ent_type(x);
     const bool tun = S.tun;
     if (ent_is_data(x)) {

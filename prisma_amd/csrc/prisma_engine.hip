@@ -103,6 +103,7 @@ prisma_step_kernel_t(KParams P) {
     Sim S;
     sim_bind(S, lv, lds, P.topo, P.log + (size_t)r * LC.log_cap * LC.rec_bytes, LC.replica_base + (uint32_t)r, lane);
     S.tun = TUN;
+    if (TUN) S.ring = (uint32_t*)(P.state + (size_t)r * LC.state_bytes + LC.s_ring);   // HBM FIFOs
     event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P, S, R, r);
     stage_out(lds, P, r, lane, R);
 }
@@ -383,6 +384,49 @@ static int plan_overlay(const prisma_topology_t* T, OverlayPlan& OP) {
     return PRISMA_OK;
 }
 
+// Tunnelled overlays: a switch link that no packet can ever cross gets no state.  The
+// links packets use are exactly those of the plan's control routes (every tunnel's
+// forward path -- data and pings --, every ping-back route, every echo route); with
+// their reverses (echoes and ping-backs leave on the reverse of the arrival link) they
+// are renumbered 0..E'-1 in ascending original id, so the live links of a node stay
+// contiguous and in neighbour order.  Abilene-on-GEANT: 74 -> 40 switch links, so with
+// the 23 access links one register slot per lane holds them all (LS = 1: 4 waves per
+// SIMD, 16 replicas per CU instead of 8).  Nothing outside the engine sees link ids.
+// Access-link tx times depend on the PHYSICAL degree and are computed before this.
+static void compact_links(const prisma_topology_t* T, OverlayPlan& OP, prisma_topology_t& TC,
+                          std::vector<int32_t>& row, std::vector<int32_t>& dst, std::vector<int32_t>& rev) {
+    const int N = T->n_nodes, E = T->n_links;
+    std::vector<char> live(E, 0);
+    for (const auto* ps : { &OP.cpaths, &OP.epaths })
+        for (const auto& p : *ps)
+            for (int l : p) { live[l] = 1; live[T->link_rev[l]] = 1; }
+    std::vector<int32_t> m(E, -1);
+    int E2 = 0;
+    for (int l = 0; l < E; ++l)
+        if (live[l]) m[l] = E2++;
+    row.assign(N + 1, 0);
+    dst.resize(E2);
+    rev.resize(E2);
+    for (int u = 0; u < N; ++u) {
+        row[u + 1] = row[u];
+        for (int l = T->row_ptr[u]; l < T->row_ptr[u + 1]; ++l)
+            if (live[l]) { dst[m[l]] = T->link_dst[l]; rev[m[l]] = m[T->link_rev[l]]; row[u + 1]++; }
+    }
+    for (auto& ti : OP.tinfo) ti = (ti & ~255u) | (uint32_t)m[ti & 255u];
+    for (auto& r : OP.route) {                   // a route over a dead link is never taken
+        const uint32_t h = r & 255u;
+        if (h != 255u) r = (r & ~255u) | (m[h] >= 0 ? (uint32_t)m[h] : 255u);
+    }
+    for (auto* ps : { &OP.cpaths, &OP.epaths })
+        for (auto& p : *ps)
+            for (int& l : p) l = m[l];
+    TC = *T;
+    TC.n_links = E2;
+    TC.row_ptr = row.data();
+    TC.link_dst = dst.data();
+    TC.link_rev = rev.data();
+}
+
 // Memory-resident engine (prisma_engine_mem.hip, identity overlays): topology as
 // variable-size arrays; state image = LDS part (header, counters, pending obs,
 // event-tree levels 1-2, link leaf keys) + HBM part (link records, flow leaf keys,
@@ -454,13 +498,13 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
 
 static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, Layout& L,
                         std::vector<unsigned char>& topo) {
-    const int N = T->n_nodes, E = T->n_links, F = T->n_flows;
+    const int N = T->n_nodes, E0 = T->n_links, F = T->n_flows;
     if (N < 2 || N > 256) return set_err(PRISMA_ERR_CONFIG, "n_nodes must be in [2, 256] (8-bit node ids)");
     if (P->engine > PRISMA_ENGINE_MEMORY) return set_err(PRISMA_ERR_CONFIG, "engine must be PRISMA_ENGINE_AUTO, _REGISTER or _MEMORY");
-    if (E < 1 || F < 1) return set_err(PRISMA_ERR_CONFIG, "need at least one link and one flow");
+    if (E0 < 1 || F < 1) return set_err(PRISMA_ERR_CONFIG, "need at least one link and one flow");
     if (!T->row_ptr || !T->link_dst || !T->link_rev || !T->flow_src || !T->flow_dst || !T->flow_rate_bps)
         return set_err(PRISMA_ERR_ARG, "null topology array");
-    if (T->row_ptr[0] != 0 || T->row_ptr[N] != E) return set_err(PRISMA_ERR_CONFIG, "row_ptr must span [0, n_links]");
+    if (T->row_ptr[0] != 0 || T->row_ptr[N] != E0) return set_err(PRISMA_ERR_CONFIG, "row_ptr must span [0, n_links]");
     int maxdeg = 0;
     for (int u = 0; u < N; ++u) {
         int d = T->row_ptr[u + 1] - T->row_ptr[u];
@@ -470,7 +514,7 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
             int v = T->link_dst[l], rv = T->link_rev[l];
             if (v < 0 || v >= N || v == u) return set_err(PRISMA_ERR_CONFIG, "bad link_dst");
             if (l > T->row_ptr[u] && T->link_dst[l - 1] >= v) return set_err(PRISMA_ERR_CONFIG, "neighbours must be ascending");
-            if (rv < 0 || rv >= E || T->link_dst[rv] != u || rv < T->row_ptr[v] || rv >= T->row_ptr[v + 1])
+            if (rv < 0 || rv >= E0 || T->link_dst[rv] != u || rv < T->row_ptr[v] || rv >= T->row_ptr[v + 1])
                 return set_err(PRISMA_ERR_CONFIG, "bad link_rev");
         }
     }
@@ -487,6 +531,17 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
             OP.ovi[T->flow_src[f]] < 0 || OP.ovi[T->flow_dst[f]] < 0)
             return set_err(PRISMA_ERR_CONFIG, "bad flow (flows run between overlay nodes)");
     }
+    // physical degrees (access-link rates, sim.cc:403-404), then a tunnelled overlay's
+    // dead links dropped (compact_links); from here on T and E are the live links
+    std::vector<int> pdeg(N);
+    for (int u = 0; u < N; ++u) pdeg[u] = T->row_ptr[u + 1] - T->row_ptr[u];
+    prisma_topology_t TC;
+    std::vector<int32_t> c_row, c_dst, c_rev;
+    if (OP.tunnels) {
+        compact_links(T, OP, TC, c_row, c_dst, c_rev);
+        T = &TC;
+    }
+    const int E = T->n_links;
     const int maxdeg_o = OP.maxdeg;
     if (P->link_bps == 0 || P->link_delay_ns < 0 || P->max_buffer_bytes == 0 || P->packet_size == 0 ||
         P->ma_size == 0 || P->ma_size > 64 || !(P->ping_interval_s > 0.0f))
@@ -518,7 +573,7 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     for (int u = 0; u < N; ++u)
         for (int l = T->row_ptr[u]; l < T->row_ptr[u + 1]; ++l) ldst[l] = T->link_dst[l];
     for (int u = 0; u < N; ++u) {
-        uint64_t bps = (uint64_t)1000000 * P->link_bps * (uint64_t)(T->row_ptr[u + 1] - T->row_ptr[u]);
+        uint64_t bps = (uint64_t)1000000 * P->link_bps * (uint64_t)pdeg[u];
         acctx[u] = sec_to_ns((double)L.data_size * 8 / (double)bps);
         ldst[E + u] = u;
     }
@@ -605,7 +660,8 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     int fs = 1, ls = 1;
     while (64 * fs < F) fs *= 2;
     while (64 * ls < (Lk > OP.T ? Lk : OP.T)) ls *= 2;
-    const uint32_t reg_lds = 4u * (uint32_t)Lk * L.WCAP * 2u + 4u * tot + 4u * (uint32_t)OP.T * L.MA +
+    const uint32_t reg_lds = 4u * (uint32_t)Lk * L.WCAP * (OP.tunnels ? 3u : 2u) + (OP.tunnels ? 0u : 4u * tot) +
+                             4u * (uint32_t)OP.T * L.MA +
                              4u * (uint32_t)(OP.tunnels ? OP.n_resp : OP.T) * L.PBK + 1024u + 16u * (1u + L.W) +
                              (uint32_t)(N * N);
     const bool reg_fits = N <= 255 && Lk <= 256 && E <= 256 && F <= 512 && OP.T <= 256 && fs <= 8 && ls <= 4 &&
@@ -657,12 +713,17 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.s_obs = take(4u * L.W);
     if (L.s_hdr != kOffHdr || L.s_cnt != kOffCnt || L.s_obs != kOffObs)
         return set_err(PRISMA_ERR_CONFIG, "internal: LDS header offsets");
+    // Tunnelled overlays keep their FIFOs in HBM (Abilene-on-GEANT: 9.6 KB of rings, sized
+    // for the control packets of every route through a link, would hold LDS at 14.8 KB per
+    // replica, 10 per CU: two rounds for 4 096 replicas) and the packet entry of each wire
+    // slot in LDS after the seqs (Sim::went), so an arrival does not read the ring.
     L.s_wt = take(4u * Lk * L.WCAP);
-    L.s_wseq = take(4u * Lk * L.WCAP);
-    L.s_ring = take(4u * tot);
+    L.s_wseq = take(4u * Lk * L.WCAP * (OP.tunnels ? 2u : 1u));
+    if (!OP.tunnels) L.s_ring = take(4u * tot);
     L.s_win = take(4u * (uint32_t)OP.T * L.MA);
     L.s_pbd = take(4u * (uint32_t)(OP.tunnels ? OP.n_resp : OP.T) * L.PBK);
     L.lds_state_bytes = o;
+    if (OP.tunnels) L.s_ring = take(4u * tot);      // HBM part of the image
     L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 19u * 64u * (uint32_t)ls));
     L.state_bytes = o;
     // Replicas per CU are bounded by LDS (160 KiB / bytes per replica) for the larger
@@ -672,7 +733,9 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     // decision reads it from HBM, L2-resident), and the DQN-buffer activations reuse the
     // table's LDS, dead in MLP launches, when it is there.
     const uint32_t tb = align16(L.table_bytes);
-    auto per_cu = [](uint32_t b) { return (160u * 1024u) / (b ? b : 1u); };
+    // (waves per CU of the step kernel: StepOcc, 4 SIMDs x its waves per SIMD)
+    const uint32_t occ = 4u * ((fs <= 2 && ls == 1) ? 4u : (ls <= 2 ? 2u : 1u));
+    auto per_cu = [occ](uint32_t b) { const uint32_t n = (160u * 1024u) / (b ? b : 1u); return n < occ ? n : occ; };
     L.table_in_lds = per_cu(L.lds_state_bytes + tb) == per_cu(L.lds_state_bytes) ? 1u : 0u;
     L.lds_bytes = L.lds_state_bytes + (L.table_in_lds ? tb : 0u);
     L.s_mlp = (L.table_in_lds && tb >= 256u) ? L.lds_state_bytes : L.lds_bytes;
