@@ -7,9 +7,9 @@ packet waiting at that node, ``done`` says it reached its destination and
 the Q-routing reward is recovered by the agent from time stamps in ``info``.
 
 ``VecRoutingEnv`` keeps that contract for R replicas at once: every replica
-always has exactly one pending forwarding decision (at whatever node the
-next data packet arrives), ``step(actions)`` applies one action per replica
-and returns the next pending decisions.  What the reference forwarder
+always has exactly one pending notification (at whatever node the next data
+packet arrives), ``step(actions)`` applies one action per replica and returns
+``(obs, reward, done, info)`` for the next notifications.  What the reference forwarder
 reconstructs from the info string — per-hop (obs, action, reward, next_obs,
 done) transitions and the loss transitions — is produced on the device by
 ``transitions()``, joined from the engine's decision log.
@@ -77,14 +77,56 @@ class VecRoutingEnv:
 
     # ------------------------------------------------------------------
     def reset(self, episode: int = 0):
+        """Start `episode` on every replica -> (obs [R, W], info) of the first notifications."""
         self.engine.reset(episode)
         self._consumed.zero_()
         obs, mask, node = self.engine.step(None)
-        return obs, {"mask": mask, "node": node}
+        return obs, self._info(obs, mask, node)[2]
 
     def step(self, actions: torch.Tensor):
+        """Apply one action per replica -> (obs, reward, done, info), each batched over replicas.
+
+        The per-node contract of Ns3Env.step (ns3env.py:417-420 -> get_state :410-415), for every
+        replica's next notification:
+          obs    int32 [R, W]: [dst, v_0..v_deg-1] of the notified packet (getObservation,
+                 data-packet-manager.cc:171-206); [1000, uid, 0..] for a small-signalling arrival
+                 (packet-routing-gym.cc:157, notify_dest with train only);
+          reward f64 [R]: the Q-routing reward of the hop that brought the notified packet here,
+                 curr_time - t_decision on the microsecond-formatted times (the value the Forwarder
+                 computes from the info string, forwarder.py:352-360; the wire's own reward field
+                 is the constant 1 of DataPacketManager::getReward, data-packet-manager.cc:219-222);
+                 0.0 for a packet's first notification, control notifications and finished episodes;
+          done   bool [R]: the notified packet is at its destination (getGameOver,
+                 data-packet-manager.cc:225-227; only with notify_dest, otherwise destination
+                 arrivals never stop the engine and done is always False);
+          info   dict: mask (uint8, 0 = the replica's episode ended this call), node (deciding node,
+                 -1 if none), uid / prev (packet uid and the record index of its previous decision,
+                 -1 if fresh), control (bool), and "transitions": every replay transition completed
+                 since the previous step (transitions(): hop transitions and loss transitions).
+        """
         obs, mask, node = self.engine.step(actions.to(device=self.device, dtype=torch.int32))
-        return obs, {"mask": mask, "node": node}
+        reward, done, info = self._info(obs, mask, node)
+        info["transitions"] = self.transitions()
+        return obs, reward, done, info
+
+    def _info(self, obs, mask, node):
+        """Reward, done and info of the current notifications, from their decision records (the
+        record of a data notification is the replica's last one, written when it was notified)."""
+        R = self.R
+        dec = self._dec_counts()
+        live = mask.to(torch.bool)
+        control = live & (obs[:, 0] == 1000)
+        data = live & ~control & (dec > 0)
+        d = (dec - 1).clamp_min(0) % self.engine.log_capacity
+        rec = decode_records(self.engine.gather_records(torch.arange(R, device=self.device, dtype=torch.int32),
+                                                        d.to(torch.int32)), self.W)
+        has_prev = data & (rec["prev"] >= 0)
+        reward = torch.where(has_prev, rec["reward"], torch.zeros_like(rec["reward"]))
+        done = data & (rec["status"] == ST_DESTINATION)
+        info = {"mask": mask, "node": node, "control": control,
+                "uid": torch.where(data, rec["uid"], torch.full_like(rec["uid"], -1)),
+                "prev": torch.where(has_prev, rec["prev"], torch.full_like(rec["prev"], -1))}
+        return reward, done, info
 
     def run(self, table: torch.Tensor, max_hops: int):
         self.engine.run(table, max_hops)

@@ -31,7 +31,7 @@ import time
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
-from google.protobuf import descriptor_pb2, descriptor_pool, message_factory
+from google.protobuf import descriptor_pb2, descriptor_pool, message_factory, struct_pb2
 
 F = descriptor_pb2.FieldDescriptorProto
 
@@ -39,6 +39,7 @@ DT_FLOAT, DT_STRING = 1, 7
 DATA_CLASS_SCALAR = 1
 FILE_VERSION = "brain.Event:2"
 CUSTOM_SCALARS_TAG = "custom_scalars__config__"
+HPARAMS_TAG = "_hparams_/session_start_info"       # tensorboard/plugins/hparams/metadata.py
 
 
 def _file() -> descriptor_pb2.FileDescriptorProto:
@@ -82,15 +83,29 @@ def _file() -> descriptor_pb2.FileDescriptorProto:
     msg("Category", [(1, "title", F.TYPE_STRING, O, None), (2, "chart", F.TYPE_MESSAGE, R, ".tensorflow.Chart"),
                      (3, "closed", F.TYPE_BOOL, O, None)])
     msg("Layout", [(1, "version", F.TYPE_INT32, O, None), (2, "category", F.TYPE_MESSAGE, R, ".tensorflow.Category")])
+    # tensorboard/plugins/hparams/plugin_data.proto (the session_start_info arm of HParamsPluginData)
+    fd.dependency.append("google/protobuf/struct.proto")
+    ssi = msg("SessionStartInfo", [(1, "hparams", F.TYPE_MESSAGE, R, ".tensorflow.SessionStartInfo.HparamsEntry"),
+                                   (2, "model_uri", F.TYPE_STRING, O, None),
+                                   (3, "monitor_url", F.TYPE_STRING, O, None),
+                                   (4, "group_name", F.TYPE_STRING, O, None),
+                                   (5, "start_time_secs", F.TYPE_DOUBLE, O, None)])
+    ent = msg("HparamsEntry", [(1, "key", F.TYPE_STRING, O, None),
+                               (2, "value", F.TYPE_MESSAGE, O, ".google.protobuf.Value")], parent=ssi)
+    ent.options.map_entry = True
+    msg("HParamsPluginData", [(1, "version", F.TYPE_INT32, O, None),
+                              (3, "session_start_info", F.TYPE_MESSAGE, O, ".tensorflow.SessionStartInfo")])
     return fd
 
 
 _pool = descriptor_pool.DescriptorPool()
+_pool.AddSerializedFile(struct_pb2.DESCRIPTOR.serialized_pb)
 _pool.AddSerializedFile(_file().SerializeToString())
 _classes = message_factory.GetMessages([_file()], pool=_pool)
 Event = _classes["tensorflow.Event"]
 Summary = _classes["tensorflow.Summary"]
 Layout = _classes["tensorflow.Layout"]
+HParamsPluginData = _classes["tensorflow.HParamsPluginData"]
 
 
 # ---------------------------------------------------------------------------
@@ -357,6 +372,60 @@ def custom_plots() -> bytes:
     return s.SerializeToString()
 
 
+def hparams_summary(params: dict, start_time_secs: Optional[float] = None, trial_id: Optional[str] = None) -> bytes:
+    """main.py:79-85 (``hp.hparams(dict_to_store)``): the session's parameters as the hparams
+    plugin's session-start summary (tag ``_hparams_/session_start_info``, plugin ``hparams``,
+    content = HParamsPluginData{version 0, session_start_info}), restated from TensorBoard's
+    hparams summary_v2 API: values go in by type (bool, then int/float as number_value, str);
+    the group name is the trial id, or the SHA-256 of the sorted-key JSON of the hparams.
+    main.py first turns the non-scalar entries (G, load_path, simArgs) into strings; this does
+    the same for any value that is not bool/int/float/str.  Parity unpinned: TensorFlow and
+    TensorBoard are not installed here, so no reference-written file could be compared."""
+    import hashlib
+    import json
+    hps = {}
+    for k, v in params.items():
+        if isinstance(v, (np.bool_,)):
+            v = bool(v)
+        elif isinstance(v, (np.integer, np.floating)):
+            v = v.item()
+        elif v is None or not isinstance(v, (bool, int, float, str)):
+            v = str(v)
+        hps[str(k)] = v
+    pd = HParamsPluginData(version=0)
+    si = pd.session_start_info
+    si.start_time_secs = time.time() if start_time_secs is None else float(start_time_secs)
+    si.group_name = trial_id if trial_id is not None else hashlib.sha256(
+        json.dumps(hps, sort_keys=True).encode("utf-8")).hexdigest()
+    for k in sorted(hps):
+        v = hps[k]
+        if isinstance(v, bool):
+            si.hparams[k].bool_value = v
+        elif isinstance(v, (int, float)):
+            si.hparams[k].number_value = float(v)
+        else:
+            si.hparams[k].string_value = v
+    s = Summary()
+    val = s.value.add(tag=HPARAMS_TAG)
+    val.metadata.plugin_data.plugin_name = "hparams"
+    val.metadata.plugin_data.content = pd.SerializeToString()
+    val.tensor.dtype = DT_FLOAT
+    val.tensor.tensor_shape.SetInParent()
+    return s.SerializeToString()
+
+
+def read_hparams(summary_bytes: bytes) -> dict:
+    """Inverse of hparams_summary for tests: {name: value} of the session-start info."""
+    s = Summary.FromString(summary_bytes)
+    v = [x for x in s.value if x.tag == HPARAMS_TAG][0]
+    pd = HParamsPluginData.FromString(v.metadata.plugin_data.content)
+    out = {}
+    for k, val in pd.session_start_info.hparams.items():
+        kind = val.WhichOneof("kind")
+        out[k] = getattr(val, kind)
+    return out
+
+
 def _mean(x: List[float]) -> float:
     return float(np.mean(np.array(x, dtype=np.float64))) if len(x) else float("nan")
 
@@ -429,11 +498,15 @@ def stats_writer_test(results_path: str, A: AgentStats, load_factor: float, mode
 
 class SessionWriters:
     """main.py:71-90: the parent, session and nb_{arrived,new,lost}_pkts writers, with the
-    custom-scalars layout written once at step 0.  Directory names follow
+    session's hparams record (when given) and the custom-scalars layout written once at step 0.  Directory names follow
     argument_parser.py's logs layout (<logs_folder>/stats, /nb_arrived_pkts, ...)."""
 
-    def __init__(self, logs_folder: str):
+    def __init__(self, logs_folder: str, hparams: Optional[dict] = None):
         self.parent = EventFileWriter(logs_folder)
+        if hparams is not None:                     # main.py:79-85, a writer of its own on logs_folder
+            hw = EventFileWriter(logs_folder)
+            hw.raw_summary(hparams_summary(hparams), step=0)
+            hw.close()
         self.session = EventFileWriter(os.path.join(logs_folder, "stats"))
         self.arrived = EventFileWriter(os.path.join(logs_folder, "nb_arrived_pkts"))
         self.new = EventFileWriter(os.path.join(logs_folder, "nb_new_pkts"))

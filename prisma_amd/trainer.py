@@ -226,8 +226,8 @@ def train(env, trainer: QRoutingTrainer, steps: int, train_every: int = 1, sync_
     losses = []
     for s in range(steps):
         a = trainer.act(obs, info["node"])
-        obs, info = env.step(a)
-        trainer.observe(env.transitions())
+        obs, _, _, info = env.step(a)
+        trainer.observe(info["transitions"])
         if s % train_every == 0:
             per = trainer.train_step()
             if per is not None:

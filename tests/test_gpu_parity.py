@@ -243,8 +243,8 @@ def test_vec_env_transitions_match_oracle_join(oracle_mod):
     got = {k: [] for k in ("obs", "action", "reward", "next_obs", "done", "replica")}
     for _ in range(300):
         a = pol.act(obs, info["node"].clamp_min(0))
-        obs, info = env.step(a)
-        tr = env.transitions()
+        obs, _, _, info = env.step(a)
+        tr = info["transitions"]
         for k in got:
             got[k].append(tr[k].cpu().numpy())
     got = {k: np.concatenate(v) for k, v in got.items()}
@@ -262,6 +262,51 @@ def test_vec_env_transitions_match_oracle_join(oracle_mod):
         assert key(got["obs"][sel].astype(np.uint32), got["action"][sel], got["reward"][sel],
                    got["next_obs"][sel].astype(np.uint32), got["done"][sel]) == \
             key(ref["obs"], ref["action"], ref["reward"], ref["next_obs"], ref["done"])
+    env.close()
+
+
+@pytest.mark.parametrize("notify", [0, 1])
+def test_vec_env_gym_step_matches_oracle(oracle_mod, notify):
+    """VecRoutingEnv.step -> (obs, reward, done, info) per replica, as Ns3Env.step hands them to
+    a node's agent (ns3env.py:417-420): obs, the hop reward forwarder.py:360 computes for the
+    notified packet, done = getGameOver; checked against the oracle stepped with the same actions."""
+    from prisma_amd.env import VecRoutingEnv
+    R = 4
+    env = VecRoutingEnv("abilene", 0, 1.5, n_replicas=R, sim_time_s=3.0, ping_as_obs=1,
+                        notify_dest=notify, train=notify)
+    orcs = [oracle_mod.OracleSim(env.topo, env.params, replica=r) for r in range(R)]
+    ref_obs = [o.step(-1) for o in orcs]
+    obs, info = env.reset()
+    rng = np.random.default_rng(7)
+    n_done = n_rew = n_ctrl = n_tr = 0
+    reward = done = None
+    for s in range(1200):
+        g, m, nd = obs.cpu().numpy(), info["mask"].cpu().numpy(), info["node"].cpu().numpy()
+        acts = np.zeros(R, dtype=np.int32)
+        for r in range(R):
+            assert (ref_obs[r] is None) == (m[r] == 0), (s, r)
+            if ref_obs[r] is None:
+                continue
+            assert np.array_equal(ref_obs[r], g[r]), (s, r)
+            if reward is not None:
+                if g[r][0] == 1000:
+                    n_ctrl += 1
+                    assert bool(info["control"][r]) and reward[r] == 0.0 and not done[r]
+                else:
+                    rec = orcs[r].records()[-1]
+                    want_rw = float(rec["reward"]) if int(rec["prev"]) >= 0 else 0.0
+                    assert float(reward[r]) == want_rw, (s, r)
+                    assert bool(done[r]) == (int(rec["status"]) == ST_DESTINATION), (s, r)
+                    assert int(info["uid"][r]) == int(rec["uid"])
+                    n_done += int(done[r])
+                    n_rew += int(int(rec["prev"]) >= 0)
+            acts[r] = rng.integers(0, env.topo.degrees[nd[r]])
+        ref_obs = [orcs[r].step(int(acts[r])) if ref_obs[r] is not None else None for r in range(R)]
+        obs, reward, done, info = env.step(torch.from_numpy(acts).cuda())
+        reward, done = reward.cpu().numpy(), done.cpu().numpy()
+        n_tr += int(info["transitions"]["reward"].numel())
+    assert n_rew > 500 and n_tr > 500
+    assert (n_done > 0 and n_ctrl > 0) if notify else (n_done == 0 and n_ctrl == 0)
     env.close()
 
 

@@ -77,6 +77,29 @@ def test_custom_plots_layout():
         "MSE_loss_over_time", "exploaration_value_over_time", "replay_buffer_length_over_time"]
 
 
+def test_hparams_record(tmp_path):
+    """main.py:79-85: the session parameters (argument_parser.py defaults, G stringified) as the
+    hparams plugin's session-start summary in the logs folder, written once at step 0."""
+    from prisma_amd.config import parse_arguments
+    params = parse_arguments(["--load_factor", "1.5", "--pingAsObs", "0"])
+    s = tblog.Summary.FromString(tblog.hparams_summary(params, start_time_secs=12.5))
+    (v,) = s.value
+    assert v.tag == "_hparams_/session_start_info" and v.metadata.plugin_data.plugin_name == "hparams"
+    pd = tblog.HParamsPluginData.FromString(v.metadata.plugin_data.content)
+    assert pd.version == 0 and pd.session_start_info.start_time_secs == 12.5
+    assert len(pd.session_start_info.group_name) == 64
+    hp = tblog.read_hparams(s.SerializeToString())
+    assert set(hp) == set(params)
+    assert hp["load_factor"] == 1.5 and hp["pingAsObs"] == 0 and hp["agent_type"] == "dqn_buffer"
+    assert hp["topology_name"] == "abilene" and isinstance(hp["topology"], str)
+    W = tblog.SessionWriters(str(tmp_path / "logs"), hparams=params)
+    W.close()
+    files = sorted(os.listdir(tmp_path / "logs"))
+    tags = [t for f in files if f.startswith("events") for e in tblog.read_events(str(tmp_path / "logs" / f))
+            for t, _, _ in e["values"]]
+    assert sorted(tags) == ["_hparams_/session_start_info", "custom_scalars__config__"]
+
+
 def _stream(oracle_mod, topo, params, n):
     """(node, obs, done, info, action) for the first n notifications, SP decisions."""
     o = oracle_mod.OracleSim(topo, params)
