@@ -151,6 +151,7 @@ struct Regs {
     LA<LS> pav_lo, pav_hi;                       // ping window mean (double), refreshed per ping-back
     LA<LS> od_lo, od_hi;                         // send time (s) of round lo
     static constexpr int NF = 4, NL = 19;
+    static constexpr bool kLazy = true;          // empty-queue transmit completions elided (lazy_resolve)
     // not staged: each lane's earliest flow (time, seq, code), refreshed when one of its flows
     // changes (flow_set, ~0.3 per hop) instead of on every event selection (~2.6 per hop)
     int64_t fm_t;
@@ -179,6 +180,7 @@ struct Hot {
     uint32_t pend, over, error, stop, hops_launch;
     uint32_t ev_launch;          // events executed in this launch (the running
                                  // totals stay in the LDS header until exit)
+    uint32_t cur_seq;            // seq of the event being executed (0 at launch start)
 };
 
 
@@ -377,6 +379,7 @@ __device__ inline void hot_load(const Sim& S, Hot& H) {
     H.pend = u_ld32(&h.pend); H.over = u_ld32(&h.over); H.error = u_ld32(&h.error);
     H.stop = u_ld32(&h.stop); H.hops_launch = u_ld32(&h.hops_launch);
     H.ev_launch = 0;
+    H.cur_seq = 0;
 }
 
 template <class RS>
@@ -391,6 +394,7 @@ __device__ inline void hot_store(Sim& S, const RS& R, const Hot& H) {
         c.now_ns = H.now; c.episode = H.episode; c.ping_rounds = H.ping_rounds; c.seq = H.seq; c.uid = H.uid;
         c.dec_count = H.dec; c.error = H.error; c.episode_over = H.over;
         c.hops_total = h.hops_total; c.events_total = h.events_total;
+        c.events += H.ev_launch;
     }
 }
 
@@ -457,7 +461,8 @@ __device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, const Ho
     R.wh_seq.set(l, k.wh_seq);
     const uint32_t n0 = lo32(H.now);
     uint32_t t = 0, s = 0xffffffffu, kind = 0;
-    if (k.busy) { t = k.cp_t; s = k.cp_seq; kind = K_COMPLETE; }
+    // a completion with nothing queued behind it is not an event (lazy_resolve)
+    if (k.busy && k.n_queue) { t = k.cp_t; s = k.cp_seq; kind = K_COMPLETE; }
     if (k.n_wire) {
         const uint32_t rw = k.wh_t - n0, rt = t - n0;
         if (kind == 0 || rw < rt || (rw == rt && k.wh_seq < s)) { t = k.wh_t; s = k.wh_seq; kind = K_ARRIVE; }
@@ -465,6 +470,53 @@ __device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, const Ho
     R.lk_t.set(l, t);
     R.lk_seq.set(l, s);
     R.lk_kind.set(l, kind);
+}
+
+__device__ __forceinline__ int64_t wave_min_i64(int64_t v);
+
+// Elided completions.  A transmit completion that finds its queue empty only clears
+// `busy` (point-to-point-net-device.cc:305-336: TransmitComplete with no packet left
+// schedules nothing and consumes no event uid), so the register-resident engine keeps it
+// out of the event set (link_put) and settles it lazily: in link_send when the link is used
+// again, and for every link at once when a launch stops (lazy_resolve).  Settling counts the
+// event the reference executed (events / events_total), so every counter equals the eager
+// schedule's.  Whether an elided completion precedes the event being executed (now,
+// cur_seq): if the wire is empty, the transmitted packet's arrival -- scheduled after its
+// completion -- has run, so the completion has too; otherwise that arrival is still ahead,
+// so the completion lies within one propagation delay before the clock or one transmission
+// after it (< 2^31 ns, checked on the host) and its 32-bit time offset is exact.
+__device__ __forceinline__ bool lazy_due(uint32_t n_wire, uint32_t cp_t, uint32_t cp_seq, const Hot& H) {
+    const int32_t dt = (int32_t)(cp_t - lo32(H.now));
+    return n_wire == 0u || dt < 0 || (dt == 0 && cp_seq < H.cur_seq);
+}
+
+// Settle every elided completion that precedes the current event, or -- at the end of an
+// episode -- every one before simTime, moving the clock to the latest of them
+// (Simulator::Stop runs every event < simTime).
+template <int FS, int LS>
+__device__ __forceinline__ void lazy_resolve(const Sim& S, Regs<FS, LS>& R, Hot& H, bool episode_end) {
+    const LV& L = S.lv;
+    const uint32_t n0 = lo32(H.now);
+    const int64_t t_end = L.t_end();
+    uint32_t n = 0;
+    int64_t tmax = H.now;
+#pragma unroll
+    for (int j = 0; j < LS; ++j) {
+        const uint32_t p1 = R.p1.v[j], p2 = R.p2.v[j];
+        const int32_t dt = (int32_t)(R.cp_t.v[j] - n0);
+        const int64_t t = H.now + (int64_t)dt;
+        const bool lazy = (p2 >> 16) != 0u && (p2 & 0xffffu) == 0u;
+        const bool due = lazy && (episode_end ? ((p1 >> 16) == 0u || t < t_end)
+                                              : lazy_due(p1 >> 16, R.cp_t.v[j], R.cp_seq.v[j], H));
+        R.p2.v[j] = due ? (p2 & 0xffffu) : p2;
+        if (due && (p1 >> 16) != 0u && t > tmax) tmax = t;
+        n += (uint32_t)__builtin_popcountll(__ballot(due));
+    }
+    H.ev_launch += n;
+    if (episode_end && n) {
+        const int64_t m = -wave_min_i64(-tmax);          // times are >= 0
+        if (m > H.now) H.now = m;
+    }
 }
 
 // flow f's next send: time, seq, draw index of that send
@@ -581,6 +633,13 @@ __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l
     uint32_t size = ent_size(L, e);
     bool ok = l < (uint32_t)L.E() ? (k.qb + size <= L.qmax_bytes()) : (k.n_queue + 1u <= L.acc_qmax_pkts());
     if (!ok) return 0;
+    if (RS::kLazy) {
+        // the transmitter's completion was elided (nothing queued behind it): if it precedes
+        // the event being executed it has happened -- count it now (lazy_due)
+        const bool due = k.busy && k.n_queue == 0u && lazy_due(k.n_wire, k.cp_t, k.cp_seq, H);
+        k.busy = due ? 0u : k.busy;
+        H.ev_launch += due ? 1u : 0u;
+    }
     uint32_t cap = ring_cap(S, l), off = ring_off(S, l);
     if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
     ring_put(S, off + k.tail, e);
@@ -856,7 +915,6 @@ __device__ __forceinline__ void on_ping_round(const Sim& S, RS& R, Hot& H) {   /
     }
     H.ping_rounds = k + 1;
     // one ns-3 event per overlay node timer (the round is NO consecutive events)
-    CNT_ADD(S, events, (uint64_t)(L.NO() - 1));
     H.ev_launch += (uint32_t)(L.NO() - 1);
     H.ping_t = H.now + L.ping_period();
     H.ping_seq = first_rearm;
@@ -1435,7 +1493,7 @@ __device__ __forceinline__ uint32_t sat_offset(int64_t t, int64_t now) {
 
 template <int FS, int LS>
 __device__ __forceinline__ void select_event(const Sim& S, const Regs<FS, LS>& R, const Hot& H, int lane, int64_t& bt,
-                                             uint32_t& bc) {
+                                             uint32_t& bc, uint32_t& bs) {
     // flows and the ping timer: each lane's cached earliest (flow_min_refresh), then one offset
     int64_t ft = R.fm_t;
     uint32_t s = R.fm_s, c = R.fm_c;
@@ -1461,6 +1519,7 @@ __device__ __forceinline__ void select_event(const Sim& S, const Regs<FS, LS>& R
             win = (uint32_t)__builtin_ctzll(__ballot(tie && s == smin));
         }
         bc = rdl(c, win);
+        bs = rdl(s, win);
         return;
     }
     // every source is >= 2^32-1 ns away (or none is pending): exact 64-bit path
@@ -1484,6 +1543,7 @@ __device__ __forceinline__ void select_event(const Sim& S, const Regs<FS, LS>& R
         win = (uint32_t)__builtin_ctzll(__ballot(tie && s2 == smin));
     }
     bc = rdl(c2, win);
+    bs = rdl(s2, win);
 }
 
 // ---------------------------------------------------------------------------
@@ -1584,17 +1644,19 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
 #endif
     while (!H.stop) {
         int64_t bt;
-        uint32_t bc;
+        uint32_t bc, bs;
 #if PRISMA_TIMING
         tm_a = TM_NOW();
 #endif
-        select_event(S, R, H, lane, bt, bc);
+        select_event(S, R, H, lane, bt, bc, bs);
         if (bt >= L.t_end()) {                           // Simulator::Stop(simTime) (sim.cc:703)
+            lazy_resolve(S, R, H, true);                 // here, not after the loop: there it costs registers
             H.over = 1;
             H.stop = 1;
             break;
         }
         H.now = bt;
+        H.cur_seq = bs;
 #if PRISMA_TRACE
         if (lane == 0 && r < 8 && g_prisma_trace) {
             const unsigned int i = g_prisma_trace_n[r]++;
@@ -1604,8 +1666,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
             }
         }
 #endif
-        CNT_ADD(S, events, 1u);
-        H.ev_launch++;
+        H.ev_launch++;                                   // added to the events counter at exit
         const uint32_t kind = bc >> 28, id = bc & 0x0fffffffu;
         TM_MARK(0);
         if (kind == K_ARRIVE) {
@@ -1656,6 +1717,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
         for (int i = 0; i < 4; ++i) atomicAdd(&g_prisma_timing[16 + i], (unsigned long long)S.tmlp[i]);
     }
 #endif
+    if (!H.error) lazy_resolve(S, R, H, false);      // elided completions up to where the launch stopped
 
     hot_store(S, R, H);
     __syncthreads();

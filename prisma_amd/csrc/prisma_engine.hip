@@ -125,11 +125,16 @@ template <int FS, int LS> struct KPair {
 // which: 0 step (table / external), 1 reset, 2 step with the DQN-buffer policy;
 // tun: tunnelled-overlay instance (identity overlays run code without the tunnel paths)
 static const void* pick_kernel(int fs, int ls, int which, bool tun) {
+#ifdef PRISMA_DEV_HEADLINE
+    // register-allocation experiments only: compile the headline instance alone
+    return (fs == 2 && ls == 1 && which == 0 && !tun) ? (const void*)prisma_step_kernel_t<2, 1, false, false> : nullptr;
+#else
 #define PK(F_, L_) if (fs == F_ && ls == L_) \
     return which == 1 ? KPair<F_, L_>::reset() : (which == 2 ? KPair<F_, L_>::step_mlp(tun) : KPair<F_, L_>::step(tun));
     PK(1, 1) PK(1, 2) PK(1, 4) PK(2, 1) PK(2, 2) PK(2, 4) PK(4, 1) PK(4, 2) PK(4, 4) PK(8, 1) PK(8, 2) PK(8, 4)
 #undef PK
     return nullptr;
+#endif
 }
 
 // Gather records (replica[i], dec[i]) into a dense array: one lane per 4-byte

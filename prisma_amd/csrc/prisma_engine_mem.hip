@@ -23,6 +23,7 @@
 // store
 // ---------------------------------------------------------------------------
 struct MemSt {
+    static constexpr bool kLazy = false;         // every transmit completion is an event
     uint32_t* lrec;              // [L][RW] link records (HBM)
     uint4* fkeys;                // [F] flow leaf keys {t lo, t hi, seq, draw} (HBM)
     uint2* lkey;                 // LDS [L] link leaf keys {t lo, seq}: t = now + (t lo - lo32(now))
@@ -220,6 +221,7 @@ __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, u
 }
 
 // ---- flows ----
+__device__ __forceinline__ void lazy_resolve(const Sim&, MemSt&, Hot&, bool) {}       // no elided completions
 __device__ __forceinline__ void flow_min_refresh(const Sim&, MemSt&, const Hot&) {}   // the event tree keeps it
 __device__ __forceinline__ uint32_t flow_draw(const Sim& S, MemSt& R, uint32_t f) {
     const uint32_t leaf = R.L + f, b = leaf >> 6, li = b * 64u + (uint32_t)S.lane;
@@ -274,7 +276,7 @@ __device__ __forceinline__ uint32_t observe_links(const Sim& S, const MemSt& R, 
 
 // next event: minimum over the super-block minima and the ping timer
 __device__ __forceinline__ void select_event(const Sim& S, const MemSt& R, const Hot& H, int lane, int64_t& bt,
-                                             uint32_t& bc) {
+                                             uint32_t& bc, uint32_t& bs) {
     int64_t t = kInf;
     uint32_t s = 0xffffffffu, c = 0u;
     if ((uint32_t)lane < R.n2) {
@@ -287,6 +289,7 @@ __device__ __forceinline__ void select_event(const Sim& S, const MemSt& R, const
     const Key k = wave_min_key(t, s, c);
     bt = k.t;
     bc = k.c;
+    bs = k.s;
 }
 
 // ---------------------------------------------------------------------------
