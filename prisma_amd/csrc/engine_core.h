@@ -152,6 +152,7 @@ struct Regs {
     LA<LS> od_lo, od_hi;                         // send time (s) of round lo
     static constexpr int NF = 4, NL = 19;
     static constexpr bool kLazy = true;          // empty-queue transmit completions elided (lazy_resolve)
+    static constexpr bool kMem = false;
     // not staged: each lane's earliest flow (time, seq, code), refreshed when one of its flows
     // changes (flow_set, ~0.3 per hop) instead of on every event selection (~2.6 per hop)
     int64_t fm_t;
@@ -626,6 +627,40 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
 }
 
 // returns 1 if enqueued, 0 if dropped (a ring overflow fails the replica)
+// link_send with the link's state already fetched (the memory-resident engine's flow event
+// issues the record load early); the register-resident engine keeps the plain form below,
+// whose register allocation the by-value LinkV disturbs
+template <class RS>
+__device__ __forceinline__ int link_send_k(const Sim& S, RS& R, Hot& H, uint32_t l, uint32_t e, LinkV k) {
+    const LV& L = S.lv;
+    uint32_t size = ent_size(L, e);
+    bool ok = l < (uint32_t)L.E() ? (k.qb + size <= L.qmax_bytes()) : (k.n_queue + 1u <= L.acc_qmax_pkts());
+    if (!ok) return 0;
+    if (RS::kLazy) {
+        // the transmitter's completion was elided (nothing queued behind it): if it precedes
+        // the event being executed it has happened -- count it now (lazy_due)
+        const bool due = k.busy && k.n_queue == 0u && lazy_due(k.n_wire, k.cp_t, k.cp_seq, H);
+        k.busy = due ? 0u : k.busy;
+        H.ev_launch += due ? 1u : 0u;
+    }
+    uint32_t cap = ring_cap(S, l), off = ring_off(S, l);
+    if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
+    ring_put(S, off + k.tail, e);
+    k.tail = (k.tail + 1 == cap) ? 0 : k.tail + 1;
+    k.n_queue++;
+    k.qb += size;
+    if (!k.busy) {                                              // :643-650
+        uint32_t xi = k.txp;
+        uint32_t hx = (k.n_queue == 1) ? e : u_ld32(&S.ring[off + xi]);
+        k.txp = (xi + 1 == cap) ? 0 : xi + 1;
+        k.n_queue--;
+        k.n_wire++;
+        k.qb -= ent_size(L, hx);
+        transmit_start(S, H, l, k, xi, hx);
+    }
+    link_put(S, R, H, l, k);
+    return 1;
+}
 template <class RS>
 __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l, uint32_t e) {
     const LV& L = S.lv;
@@ -658,6 +693,7 @@ __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l
     link_put(S, R, H, l, k);
     return 1;
 }
+
 
 template <class RS>
 __device__ __forceinline__ void on_complete(const Sim& S, RS& R, Hot& H, uint32_t l) {   // :305-336
@@ -934,12 +970,26 @@ __device__ __forceinline__ void flow_next(const Sim& S, RS& R, Hot& H, uint32_t 
 
 template <class RS>
 __device__ __forceinline__ void on_flow(const Sim& S, RS& R, Hot& H, uint32_t f) {
-    uint32_t draw = flow_draw(S, R, f);
-    if (draw != 0) {                                                // SendPacket :297-358
-        uint32_t src = (uint32_t)t_fsrc(S, f);
-        uint32_t par = (uint32_t)(H.now / 1000000000) & 1u;         // start second (its parity)
-        link_send(S, R, H, (uint32_t)S.lv.E() + src, f_make((uint32_t)t_fdst(S, f), par, H.uid & kUidMask));   // access link
-        H.uid++;
+    // memory-resident engine: the access link's record is fetched first, so its load and the
+    // flow block's are in flight together (one HBM round trip)
+    uint32_t draw;
+    if constexpr (RS::kMem) {
+        const uint32_t acc = (uint32_t)S.lv.E() + (uint32_t)t_fsrc(S, f);
+        const LinkV k = link_get(R, acc);
+        draw = flow_draw(S, R, f);
+        if (draw != 0) {                                            // SendPacket :297-358
+            const uint32_t par = (uint32_t)(H.now / 1000000000) & 1u;   // start second (its parity)
+            link_send_k(S, R, H, acc, f_make((uint32_t)t_fdst(S, f), par, H.uid & kUidMask), k);
+            H.uid++;
+        }
+    } else {
+        draw = flow_draw(S, R, f);
+        if (draw != 0) {
+            const uint32_t src = (uint32_t)t_fsrc(S, f);
+            const uint32_t par = (uint32_t)(H.now / 1000000000) & 1u;
+            link_send(S, R, H, (uint32_t)S.lv.E() + src, f_make((uint32_t)t_fdst(S, f), par, H.uid & kUidMask));
+            H.uid++;
+        }
     }
     flow_next(S, R, H, f, draw);                                    // StartSending / ScheduleNextTx
 }
@@ -996,20 +1046,52 @@ struct MlpPre {
     float4 w2[16], w3[16], w4[16];
     float b2, b3, b4;
 };
+// what the memory-resident engine's arrival handler fetches for the decision that follows
+// (layer 1's buffer-branch chunks and bias, layer 2): it rides along the arrival's second
+// round trip, and layers 3-4 load while layers 1-2 compute
+struct MlpPre1 {
+    float4 w2[16];
+    float b2;
+    float4 wb[4];
+    float b1v;
+};
 
-__device__ __forceinline__ void mlp_preload(MlpPre& M, const float* __restrict__ RP, int lane, int D, int deg) {
-    const float4* __restrict__ W2 = (const float4*)RP;
+__device__ __forceinline__ void mlp_preload(MlpPre& M, const float* __restrict__ RP, int lane, int D, int deg,
+                                            bool l2 = true) {
+    const float4* __restrict__ W2 = l2 ? (const float4*)RP : nullptr;
     const float4* __restrict__ W3 = (const float4*)(RP + mlp_rp_layer_floats(64));
     const float4* __restrict__ W4 = (const float4*)(RP + 2 * mlp_rp_layer_floats(64));
+    if (W2) {
 #pragma unroll
-    for (int c = 0; c < 16; ++c) M.w2[c] = W2[c * 64 + lane];
+        for (int c = 0; c < 16; ++c) M.w2[c] = W2[c * 64 + lane];
+        M.b2 = RP[64 * 64 + lane];
+    }
 #pragma unroll
     for (int c = 0; c < 16; ++c) M.w3[c] = W3[c * 64 + lane];
 #pragma unroll
     for (int c = 0; c < 16; ++c) M.w4[c] = lane < deg ? W4[c * D + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-    M.b2 = RP[64 * 64 + lane];
     M.b3 = RP[mlp_rp_layer_floats(64) + 64 * 64 + lane];
     M.b4 = lane < deg ? RP[2 * mlp_rp_layer_floats(64) + 64 * D + lane] : 0.0f;
+}
+
+// every weight a decision at node v reads except its one-hot row (which needs the
+// destination): issued by the memory-resident engine's arrival handler together with
+// its second round trip (previous decision record, observation), so the decision finds
+// them in registers
+__device__ __forceinline__ void mlp_preload_node(MlpPre1& M, const Sim& S, uint32_t v) {
+    const int lane = S.lane;
+    const int D = S.lv.max_deg();
+    const float* __restrict__ RP1 = S.mlp_rp + (size_t)v * mlp_rp_node_floats(D);
+    const float* __restrict__ RP = RP1 + mlp_rp_l1_floats(D);
+    const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
+#pragma unroll
+    for (int c = 0; c < 16; ++c) M.w2[c] = ((const float4*)RP)[c * 64 + lane];
+    M.b2 = RP[64 * 64 + lane];
+    const int j32 = lane & 31, nck = (deg + 3) >> 2;
+    const float4* __restrict__ Wb4 = (const float4*)RP1;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) M.wb[c] = (c < nck) ? Wb4[c * 32 + j32] : make_float4(0.f, 0.f, 0.f, 0.f);
+    M.b1v = (lane < 32) ? RP1[128 * ((D + 3) / 4) + 32 + j32] : RP1[128 * ((D + 3) / 4) + j32];
 }
 
 __device__ __forceinline__ float mlp_dense64_pre(const Sim& S, const float4 (&w)[16], float b) {
@@ -1029,8 +1111,8 @@ __device__ __forceinline__ float mlp_dense64_pre(const Sim& S, const float4 (&w)
 // one-hot input: obs[0] (the destination's overlay index, lane 0 of obs_reg)
 __device__ __forceinline__ float rdlf(float x, uint32_t k) { return __uint_as_float(rdl(__float_as_uint(x), k)); }
 
-template <int B>
-__device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs_reg) {
+template <int B, bool PRE = false>
+__device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs_reg, const MlpPre1& P1) {
     const LV& L = S.lv;
     const int lane = S.lane;
     const int N = L.N(), D = L.max_deg();
@@ -1046,18 +1128,25 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
     const uint32_t dst = rdl(obs_reg, 0);
     MlpPre M;
-    if constexpr (B == kMlpAll) mlp_preload(M, RP, lane, D, deg);
+    if constexpr (B == kMlpAll) mlp_preload(M, RP, lane, D, deg, !PRE);   // PRE: layer 2 came with the arrival
     // layer-1 weights first (independent of the normalisation): one W1 row element and
     // b1 for the one-hot branch (lanes 0-31), the Wb chunks and bb for the buffers branch
     // (lanes 32-63; deg <= D, so at most ceil(D/4) chunks)
     const int j32 = lane & 31;
     const int nck = (deg + 3) >> 2;
     const float4* __restrict__ Wb4 = (const float4*)RP1;
-    const float b1v = (lane < 32) ? RP1[128 * ((D + 3) / 4) + 32 + j32] : RP1[128 * ((D + 3) / 4) + j32];
     const float w1v = (lane < 32) ? W1[((int)v * N + (int)dst) * 32 + j32] : 0.0f;
+    float b1v;
     float4 wb[4];
+    if constexpr (PRE) {
+        b1v = P1.b1v;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) wb[c] = (c < nck) ? Wb4[c * 32 + j32] : make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int c = 0; c < 4; ++c) wb[c] = P1.wb[c];
+    } else {
+        b1v = (lane < 32) ? RP1[128 * ((D + 3) / 4) + 32 + j32] : RP1[128 * ((D + 3) / 4) + j32];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wb[c] = (c < nck) ? Wb4[c * 32 + j32] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     // LayerNormalization of the deg buffer values (population variance, epsilon 1e-3):
     // lane k+1 holds buffer value k; sums run in k order through readlanes
     const float xf = (float)obs_reg;
@@ -1092,7 +1181,8 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
     TM_MLP(0);
-    if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w2, M.b2));
+    if constexpr (PRE) h = det_elu(mlp_dense64_pre(S, P1.w2, P1.b2));
+    else if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w2, M.b2));
     else h = det_elu(mlp_dense64<B>(S, RP, lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
@@ -1212,8 +1302,9 @@ __device__ __forceinline__ uint32_t pbd_slot(const Sim& S, uint32_t t, uint32_t 
 }
 
 // returns 1 if a data decision needs an action
-template <class RS>
-__device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l, Decision& D, bool fused) {
+template <bool PRE = false, class RS>
+__device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l, Decision& D, bool fused,
+                                         MlpPre1& Mpre) {
     const LV& L = S.lv;
     const uint32_t v = (uint32_t)t_ldst(S, l);
     LinkV k = link_get(R, l);
@@ -1238,6 +1329,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap() - 1)) * L.rec_bytes();
         const uint4 ph = *(const uint4*)pr;
         const uint2 pw = *(const uint2*)(pr + 24);
+        if constexpr (PRE) mlp_preload_node(Mpre, S, v);          // the decision's weights ride along
         // memory-resident engine: the observation's gather goes out with the record
         // load, before the arrival link's update (it reads node v's out-links, which
         // nothing touches before the decision)
@@ -1616,7 +1708,8 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
     if (H.pend && !H.over) {
         if (table_mode) {
             uint32_t pn = u_ld32(&S.h->pend_node), pd = u_ld32(&S.h->pend_ent[1]);
-            const int a = mlp_mode ? mlp_action<MB>(S, pn, (lane < L.W()) ? S.obs[lane] : 0u)
+            MlpPre1 M0;
+            const int a = mlp_mode ? mlp_action<MB>(S, pn, (lane < L.W()) ? S.obs[lane] : 0u, M0)
                                    : table_action(S, pn * NN + pd);
             H.hops_launch += finish_pending(S, R, H, a);
         } else if (P.actions) {
@@ -1642,6 +1735,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
 #else
 #define TM_MARK(i) do { } while (0)
 #endif
+    constexpr bool kPre = MLP && RS::kMem;               // memory-resident engine + MLP: weights prefetched
     while (!H.stop) {
         int64_t bt;
         uint32_t bc, bs;
@@ -1671,11 +1765,12 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
         TM_MARK(0);
         if (kind == K_ARRIVE) {
             Decision D;
-            const int need = on_arrive(S, R, H, id, D, table_mode);
+            MlpPre1 Mp;                                  // (kPre) the decision's first weights, fetched on arrival
+            const int need = on_arrive<kPre>(S, R, H, id, D, table_mode, Mp);
             TM_MARK(1);
             if (need) {
                 if (table_mode) {
-                    const int a = mlp_mode ? mlp_action<MB>(S, D.v, D.obs)
+                    const int a = mlp_mode ? mlp_action<MB, kPre>(S, D.v, D.obs, Mp)
                                            : table_action(S, D.v * NN + D.dst);
                     apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, a, true,
                                    D.reward, D.prev, D.obs,

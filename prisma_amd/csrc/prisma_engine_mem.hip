@@ -23,7 +23,8 @@
 // store
 // ---------------------------------------------------------------------------
 struct MemSt {
-    static constexpr bool kLazy = false;         // every transmit completion is an event
+    static constexpr bool kLazy = true;          // empty-queue transmit completions elided (lazy_resolve)
+    static constexpr bool kMem = true;
     uint32_t* lrec;              // [L][RW] link records (HBM)
     uint4* fkeys;                // [F] flow leaf keys {t lo, t hi, seq, draw} (HBM)
     uint2* lkey;                 // LDS [L] link leaf keys {t lo, seq}: t = now + (t lo - lo32(now))
@@ -211,7 +212,7 @@ __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, u
     // next event of the link (register-resident link_put's rule)
     const uint32_t n0 = lo32(H.now);
     uint32_t t = 0, s = 0xffffffffu, kind = 0;
-    if (k.busy) { t = k.cp_t; s = k.cp_seq; kind = K_COMPLETE; }
+    if (k.busy && k.n_queue) { t = k.cp_t; s = k.cp_seq; kind = K_COMPLETE; }   // (lazy_resolve)
     if (k.n_wire) {
         const uint32_t rw = k.wh_t - n0, rt = t - n0;
         if (kind == 0 || rw < rt || (rw == rt && k.wh_seq < s)) { t = k.wh_t; s = k.wh_seq; kind = K_ARRIVE; }
@@ -221,7 +222,6 @@ __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, u
 }
 
 // ---- flows ----
-__device__ __forceinline__ void lazy_resolve(const Sim&, MemSt&, Hot&, bool) {}       // no elided completions
 __device__ __forceinline__ void flow_min_refresh(const Sim&, MemSt&, const Hot&) {}   // the event tree keeps it
 __device__ __forceinline__ uint32_t flow_draw(const Sim& S, MemSt& R, uint32_t f) {
     const uint32_t leaf = R.L + f, b = leaf >> 6, li = b * 64u + (uint32_t)S.lane;
@@ -258,6 +258,38 @@ __device__ __forceinline__ void ping_set_win(const Sim& S, MemSt& R, uint32_t t,
     const uint32_t j = threadIdx.x;
     if (j == LR_PMWIN || j == LR_PAVLO || j == LR_PAVHI)
         R.lrec[t * R.RW + j] = j == LR_PMWIN ? win : (j == LR_PAVLO ? (uint32_t)avg : (uint32_t)(avg >> 32));
+}
+
+// Elided completions (engine_core.h lazy_due): settle every one that precedes the current
+// event -- or, at the end of an episode, every one before simTime -- with lane i scanning
+// links i, 64 + i, ... (a few dozen dependent loads per launch).  This is the only place
+// where a lane other than LR_P2 stores word LR_P2 of a record; the next access to it is
+// by the same lane (a later scan of this launch) or in a later launch.
+__device__ __forceinline__ void lazy_resolve(const Sim& S, MemSt& R, Hot& H, bool episode_end) {
+    const uint32_t n0 = lo32(H.now);
+    const int64_t t_end = S.lv.t_end();
+    uint32_t n = 0;
+    int64_t tmax = H.now;
+    for (uint32_t b = 0; b < R.L; b += 64u) {
+        const uint32_t l = b + (uint32_t)S.lane;
+        bool due = false;
+        if (l < R.L) {
+            uint32_t* p = R.lrec + l * R.RW;
+            const uint32_t p1 = p[LR_P1], p2 = p[LR_P2], cpt = p[LR_CPT], cps = p[LR_CPS];
+            const int32_t dt = (int32_t)(cpt - n0);
+            const int64_t t = H.now + (int64_t)dt;
+            const bool lazy = (p2 >> 16) != 0u && (p2 & 0xffffu) == 0u;
+            due = lazy && (episode_end ? ((p1 >> 16) == 0u || t < t_end) : lazy_due(p1 >> 16, cpt, cps, H));
+            if (due) p[LR_P2] = p2 & 0xffffu;
+            if (due && (p1 >> 16) != 0u && t > tmax) tmax = t;
+        }
+        n += (uint32_t)__builtin_popcountll(__ballot(due));
+    }
+    H.ev_launch += n;
+    if (episode_end && n) {
+        const int64_t m = -wave_min_i64(-tmax);
+        if (m > H.now) H.now = m;
+    }
 }
 
 // observation of node v: lane i (1 <= i <= deg) gathers the words of link ovrow[v] + i - 1
