@@ -84,7 +84,10 @@ template <int FS, int LS> struct StepOcc {
 #ifndef PRISMA_MLP_B_WIDE
 #define PRISMA_MLP_B_WIDE 8
 #endif
-    static constexpr int mlp_batch = waves >= 4 ? 4 : PRISMA_MLP_B_WIDE;   // DQN-buffer loads in flight
+#ifndef PRISMA_MLP_B_NARROW
+#define PRISMA_MLP_B_NARROW 4
+#endif
+    static constexpr int mlp_batch = waves >= 4 ? PRISMA_MLP_B_NARROW : PRISMA_MLP_B_WIDE;   // DQN-buffer loads in flight
 };
 
 // MLP: the in-kernel DQN-buffer policy is compiled in (mode 4 only); the table /
