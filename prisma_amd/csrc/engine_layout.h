@@ -107,9 +107,11 @@ struct TopoImage {
     uint32_t tinfo[256];         // tunnel t: first link | target << 8 | origin << 16 | links << 24
     int32_t ovi[256];            // overlay index of node x (obs[0] of a packet for x), -1 if none
     int32_t ovnode[256];         // underlay id of overlay node i (ping timers, overlay order)
-    uint32_t rinfo[256];         // tunnelled overlays: ring of link l = entries [off, off + cap): off | cap << 16
+    uint32_t rinfo[256];         // ring of link l = entries [off, off + cap): off | cap << 16
     uint32_t tresp[256];         // tunnelled overlays: ping-back delay slot base of tunnel t | responder
                                  // position mask << 16 (overlay nodes on the tunnel, target included)
+    uint32_t ctx[8];             // transmission time on a switch link of an entry of class
+                                 // (type | echo bit << 2), ns (< 2^31)
     // uint32_t route[N][N] follows (tunnelled overlays only): next link x -> y | hops(x, y) << 8
 };
 __host__ __device__ inline uint32_t ti_link(uint32_t ti) { return ti & 255u; }

@@ -116,7 +116,7 @@ __host__ __device__ inline double ns_to_sec(int64_t t) { return (double)t / 1e9;
 // microseconds of std::to_string(GetSeconds()) (%f, ties-to-even on the
 // exact binary value) as Python reads them back (packet-manager.cc:127-128).
 __host__ __device__ inline uint64_t py_micros(int64_t t) {
-    uint64_t u = (uint64_t)(t / 1000);
+    uint64_t u = (uint64_t)t / 1000u;                   // t >= 0
     int64_t r = t - (int64_t)u * 1000;
     if (r != 500) return r < 500 ? u : u + 1;
     double x = ns_to_sec(t);

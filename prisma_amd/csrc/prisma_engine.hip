@@ -702,14 +702,18 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     memcpy(TI.tinfo, OP.tinfo.data(), 4u * OP.T);
     for (int x = 0; x < N; ++x) TI.ovi[x] = OP.ovi[x];
     memcpy(TI.ovnode, OP.ovnode.data(), 4u * OP.NO);
-    if (OP.tunnels) {
+    {                                                // ring of every link (engine_core.h ring_off)
         uint32_t off = 0;
         for (int l = 0; l < Lk; ++l) {
             const uint32_t cap = l < E ? rcap[l] : L.qcap_a;
             TI.rinfo[l] = off | (cap << 16);
             off += cap;
         }
-        memcpy(TI.tresp, OP.tresp.data(), 4u * OP.T);
+    }
+    if (OP.tunnels) memcpy(TI.tresp, OP.tresp.data(), 4u * OP.T);
+    for (uint32_t c = 0; c < 8; ++c) {               // entry classes: relay, fresh, ping fwd, ping back, +echo bit
+        const bool data = (c & 2u) == 0u, echo = c == 7u;
+        TI.ctx[c] = (uint32_t)(data ? L.sw_txd : (echo ? L.sw_txe : L.sw_txp));
     }
     if (OP.tunnels) memcpy(topo.data() + sizeof(TopoImage), OP.route.data(), 4u * (size_t)N * N);
 
