@@ -291,6 +291,7 @@ struct Sim {
     bool tun;                               // tunnelled overlay: a compile-time constant in the
                                             // step kernels (template TUN), folded after inlining
     bool mem;                               // memory-resident engine (compile-time constant, folded)
+    bool ctrl;                              // --train echo / notify_dest paths compiled in (constant)
     // memory-resident engine: variable-size topology arrays (scalar loads)
     const CAS int32_t* m_rowptr;
     const CAS int32_t* m_ldst;
@@ -331,6 +332,7 @@ __device__ inline void sim_bind(Sim& S, const LV& L, unsigned char* lds, const u
     S.lane = lane;
     S.tun = L.tunnels() != 0u;
     S.mem = false;
+    S.ctrl = true;
     S.lrec = nullptr;
 }
 
@@ -928,13 +930,13 @@ __device__ __forceinline__ int finish_pending(const Sim& S, RS& R, Hot& H, int a
     const Hdr& h = *S.h;
     H.pend = 0;
     const uint32_t x = u_ld32(&h.pend_ent[0]), flags = u_ld32(&h.pend_ent[3]);
-    if (flags & PEND_CTRL) {
+    if (S.ctrl && (flags & PEND_CTRL)) {
         receive_counters(S, R, H, x, false, 0u);
         return 0;
     }
-    const uint32_t echo_link = (flags & PEND_ECHO) ? (uint32_t)t_lrev(S, u_ld32(&h.pend_link)) : kNoLink;
+    const uint32_t echo_link = (S.ctrl && (flags & PEND_ECHO)) ? (uint32_t)t_lrev(S, u_ld32(&h.pend_link)) : kNoLink;
     const uint32_t last = u_ld32(&h.pend_last);
-    if (flags & PEND_DEST) {
+    if (S.ctrl && (flags & PEND_DEST)) {
         if (echo_link != kNoLink) send_echo(S, R, H, echo_link, u_ld32(&h.pend_uid), last);
         receive_counters(S, R, H, x, true, u_ld32(&h.pend_ent[2]));
         return 0;
@@ -1412,12 +1414,12 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         CNT_ADD(S, decisions, 1u);
         // --train: the answer to this notification also echoes a small-signalling
         // packet to the last hop, unless this node is the packet's source (:303-306)
-        const uint32_t echo = (L.train() && v != ent_src(x, v)) ? PEND_ECHO : 0u;
+        const uint32_t echo = (S.ctrl && L.train() && v != ent_src(x, v)) ? PEND_ECHO : 0u;
         D.x = x; D.dst = dst; D.start = start; D.uid = uid; D.v = v; D.d = d; D.reward = reward; D.prev = prev;
         D.obs = o; D.flags = echo; D.last = last; D.ttl = ttl;
         if (dst == v) {                                             // getGameOver
             write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_DESTINATION, o, ttl);
-            if (!fused && L.notify_dest()) {                        // the agent is notified (done=True)
+            if (!fused && S.ctrl && L.notify_dest()) {              // the agent is notified (done=True)
                 D.flags |= PEND_DEST;
                 return 1;
             }
@@ -1429,12 +1431,12 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         return 1;
     }
     wire_pop(S, R, H, l, k);
-    if (ent_is_echo(x)) {
+    if (S.ctrl && ent_is_echo(x)) {                                 // (echoes exist only with --train)
         const uint32_t to = e_to(x);
         if (tun && to != v) { ctrl_forward(S, R, H, v, to, x); return 0; }
         // SmallSignalingPacketManager::receivePacket (small-signaling-packet-manager.cc:86-94):
         // addressed to this node, so valid -> Notify; the agent sees obs [1000]
-        if (!fused && L.notify_dest()) {
+        if (!fused && S.ctrl && L.notify_dest()) {
             D.x = x; D.v = v; D.uid = e_uid(x); D.flags = PEND_CTRL; D.last = 0u;
             D.obs = (S.lane == 0) ? 1000u : ((S.lane == 1) ? e_uid(x) : 0u);
             return 1;

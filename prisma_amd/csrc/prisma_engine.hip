@@ -36,6 +36,7 @@
 #include "numerics.h"
 
 #include "engine_core.h"
+#include "step_kernel.h"
 
 // memory-resident engine kernels (prisma_engine_mem.hip): 0 step, 1 reset, 2 step + DQN-buffer MLP
 const void* prisma_mem_kernel(int which);
@@ -76,68 +77,17 @@ __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     stage_out(lds, P, r, lane, R);
 }
 
-// waves per SIMD the register allocator must leave room for: 4 (<= 128
-// VGPRs) for small replicas so 4096 of them are resident on 256 CUs at
-// once, 2 (<= 256) up to 512 flows x 128 links
-template <int FS, int LS> struct StepOcc {
-    static constexpr int waves = (FS <= 2 && LS == 1) ? 4 : (LS <= 2 ? 2 : 1);
-#ifndef PRISMA_MLP_B_WIDE
-#define PRISMA_MLP_B_WIDE 8
-#endif
-#ifndef PRISMA_MLP_B_NARROW
-#define PRISMA_MLP_B_NARROW 4
-#endif
-    static constexpr int mlp_batch = waves >= 4 ? PRISMA_MLP_B_NARROW : PRISMA_MLP_B_WIDE;   // DQN-buffer loads in flight
-};
+// step kernels (step_kernel.h): the instances with the --train / notify_dest code paths
+// are compiled here, the ones without them in prisma_engine_lite.hip
+const void* prisma_pick_step_lite(int fs, int ls, bool mlp, bool tun);
+static const void* pick_step_ctrl(int fs, int ls, bool mlp, bool tun) { return pick_step<true>(fs, ls, mlp, tun); }
 
-// MLP: the in-kernel DQN-buffer policy is compiled in (mode 4 only); the table /
-// external instances carry none of its code or registers.
-template <int FS, int LS, bool MLP, bool TUN>
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(StepOcc<FS, LS>::waves)))
-prisma_step_kernel_t(KParams P) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const int r = blockIdx.x, lane = threadIdx.x;
-    CLayout& LC = *(CLayout*)P.lay;
-    LV lv;
-    lv.load(P.lay, lane);
-    Regs<FS, LS> R;
-    stage_in(lds, P, r, lane, R);
-    __syncthreads();
-    Sim S;
-    sim_bind(S, lv, lds, P.topo, P.log + (size_t)r * LC.log_cap * LC.rec_bytes, LC.replica_base + (uint32_t)r, lane);
-    S.tun = TUN;
-    if (TUN) S.ring = (uint32_t*)(P.state + (size_t)r * LC.state_bytes + LC.s_ring);   // HBM FIFOs
-    event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P, S, R, r);
-    stage_out(lds, P, r, lane, R);
-}
-
-// instantiations: flow slots FS in {1,2,4,8} (F <= 512), link slots LS in {1,2,4} (L <= 256)
-typedef void (*kernel_fn)(KParams);
-template <int FS, int LS> struct KPair {
-    static const void* step(bool tun) {
-        return tun ? (const void*)prisma_step_kernel_t<FS, LS, false, true>
-                   : (const void*)prisma_step_kernel_t<FS, LS, false, false>;
-    }
-    static const void* step_mlp(bool tun) {
-        return tun ? (const void*)prisma_step_kernel_t<FS, LS, true, true>
-                   : (const void*)prisma_step_kernel_t<FS, LS, true, false>;
-    }
-    static const void* reset() { return (const void*)prisma_reset_kernel_t<FS, LS>; }
-};
-
-// which: 0 step (table / external), 1 reset, 2 step with the DQN-buffer policy;
-// tun: tunnelled-overlay instance (identity overlays run code without the tunnel paths)
-static const void* pick_kernel(int fs, int ls, int which, bool tun) {
-#ifdef PRISMA_DEV_HEADLINE
-    // register-allocation experiments only: compile the headline instance alone
-    return (fs == 2 && ls == 1 && which == 0 && !tun) ? (const void*)prisma_step_kernel_t<2, 1, false, false> : nullptr;
-#else
-#define PK(F_, L_) if (fs == F_ && ls == L_) \
-    return which == 1 ? KPair<F_, L_>::reset() : (which == 2 ? KPair<F_, L_>::step_mlp(tun) : KPair<F_, L_>::step(tun));
+template <int FS, int LS> const void* reset_kernel() { return (const void*)prisma_reset_kernel_t<FS, LS>; }
+static const void* pick_reset(int fs, int ls) {
+#define PK(F_, L_) if (fs == F_ && ls == L_) return reset_kernel<F_, L_>();
     PK(1, 1) PK(1, 2) PK(1, 4) PK(2, 1) PK(2, 2) PK(2, 4) PK(4, 1) PK(4, 2) PK(4, 4) PK(8, 1) PK(8, 2) PK(8, 4)
 #undef PK
     return nullptr;
-#endif
 }
 
 // Gather records (replica[i], dec[i]) into a dense array: one lane per 4-byte
@@ -800,9 +750,12 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
         e->k_reset = prisma_mem_kernel(1);
         e->k_step_mlp = prisma_mem_kernel(2);
     } else {
-        e->k_step = pick_kernel(L.FS, L.LS, 0, L.tunnels != 0u);
-        e->k_reset = pick_kernel(L.FS, L.LS, 1, false);
-        e->k_step_mlp = pick_kernel(L.FS, L.LS, 2, L.tunnels != 0u);
+        // the --train echo and notify_dest paths are compiled only into the instances that need them
+        const bool ctrl = L.train || L.notify_dest;
+        auto pick = ctrl ? pick_step_ctrl : prisma_pick_step_lite;
+        e->k_step = pick(L.FS, L.LS, false, L.tunnels != 0u);
+        e->k_reset = pick_reset(L.FS, L.LS);
+        e->k_step_mlp = pick(L.FS, L.LS, true, L.tunnels != 0u);
     }
     (void)hipFuncSetAttribute(e->k_step_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_mlp_bytes);
     (void)hipFuncSetAttribute(e->k_step, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);

@@ -1,0 +1,66 @@
+// step_kernel.h -- the register-resident engine's step kernel template and its instance table,
+// included by prisma_engine.hip (instances with the --train echo / notify_dest code, CTRL) and
+// prisma_engine_lite.hip (instances without it: the compiler allocates registers for every
+// path a kernel contains, and these rarely-taken ones cost the common case ~2 %).
+#pragma once
+#include "engine_core.h"
+
+// waves per SIMD the register allocator must leave room for: 4 (<= 128
+// VGPRs) for small replicas so 4096 of them are resident on 256 CUs at
+// once, 2 (<= 256) up to 512 flows x 128 links
+template <int FS, int LS> struct StepOcc {
+    static constexpr int waves = (FS <= 2 && LS == 1) ? 4 : (LS <= 2 ? 2 : 1);
+#ifndef PRISMA_MLP_B_WIDE
+#define PRISMA_MLP_B_WIDE 8
+#endif
+#ifndef PRISMA_MLP_B_NARROW
+#define PRISMA_MLP_B_NARROW 4
+#endif
+    static constexpr int mlp_batch = waves >= 4 ? PRISMA_MLP_B_NARROW : PRISMA_MLP_B_WIDE;   // DQN-buffer loads in flight
+};
+
+// MLP: the in-kernel DQN-buffer policy is compiled in (mode 4 only); the table /
+// external instances carry none of its code or registers.  CTRL: the --train echo and
+// notify_dest paths are compiled in (used when either is set).
+template <int FS, int LS, bool MLP, bool TUN, bool CTRL>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(StepOcc<FS, LS>::waves)))
+prisma_step_kernel_t(KParams P) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const int r = blockIdx.x, lane = threadIdx.x;
+    CLayout& LC = *(CLayout*)P.lay;
+    LV lv;
+    lv.load(P.lay, lane);
+    Regs<FS, LS> R;
+    stage_in(lds, P, r, lane, R);
+    __syncthreads();
+    Sim S;
+    sim_bind(S, lv, lds, P.topo, P.log + (size_t)r * LC.log_cap * LC.rec_bytes, LC.replica_base + (uint32_t)r, lane);
+    S.tun = TUN;
+    S.ctrl = CTRL;
+    if (TUN) S.ring = (uint32_t*)(P.state + (size_t)r * LC.state_bytes + LC.s_ring);   // HBM FIFOs
+    event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P, S, R, r);
+    stage_out(lds, P, r, lane, R);
+}
+
+// instantiations: flow slots FS in {1,2,4,8} (F <= 512), link slots LS in {1,2,4} (L <= 256)
+template <int FS, int LS, bool CTRL> const void* step_kernel(bool mlp, bool tun) {
+    if (mlp) return tun ? (const void*)prisma_step_kernel_t<FS, LS, true, true, CTRL>
+                        : (const void*)prisma_step_kernel_t<FS, LS, true, false, CTRL>;
+    return tun ? (const void*)prisma_step_kernel_t<FS, LS, false, true, CTRL>
+               : (const void*)prisma_step_kernel_t<FS, LS, false, false, CTRL>;
+}
+
+// tun: tunnelled-overlay instance (identity overlays run code without the tunnel paths)
+template <bool CTRL>
+static const void* pick_step(int fs, int ls, bool mlp, bool tun) {
+#ifdef PRISMA_DEV_HEADLINE
+    // register-allocation experiments only: compile the headline instance alone
+    return (!CTRL && fs == 2 && ls == 1 && !mlp && !tun) ? (const void*)prisma_step_kernel_t<2, 1, false, false, false>
+                                                         : nullptr;
+#else
+#define PK(F_, L_) if (fs == F_ && ls == L_) return step_kernel<F_, L_, CTRL>(mlp, tun);
+    PK(1, 1) PK(1, 2) PK(1, 4) PK(2, 1) PK(2, 2) PK(2, 4) PK(4, 1) PK(4, 2) PK(4, 4) PK(8, 1) PK(8, 2) PK(8, 4)
+#undef PK
+    return nullptr;
+#endif
+}

@@ -218,9 +218,10 @@ class PrismaEngine:
             while 64 * ls < max(topo.n_links + topo.n_nodes, topo.n_tunnels):
                 ls *= 2
             tun = "false" if topo.identity else "true"
-            # the third template argument is the in-kernel MLP
-            self.kernel_name = f"prisma_step_kernel_t<{fs}, {ls}, false, {tun}>"
-            self.kernel_name_mlp = f"prisma_step_kernel_t<{fs}, {ls}, true, {tun}>"
+            ctrl = "true" if (params.get("train") or params.get("notify_dest")) else "false"
+            # template arguments: slots, in-kernel MLP, tunnels, --train/notify_dest paths
+            self.kernel_name = f"prisma_step_kernel_t<{fs}, {ls}, false, {tun}, {ctrl}>"
+            self.kernel_name_mlp = f"prisma_step_kernel_t<{fs}, {ls}, true, {tun}, {ctrl}>"
         self.obs = torch.zeros((self.R, self.W), dtype=torch.int32, device=self.torch_device)
         self.mask = torch.zeros(self.R, dtype=torch.uint8, device=self.torch_device)
         self.node = torch.zeros(self.R, dtype=torch.int32, device=self.torch_device)

@@ -16,7 +16,7 @@ NAMES = ["select", "arrive", "decision", "complete", "flow", "ping_round", "dec:
 if sys.argv[1] == "build":
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     objs = []
-    for f in ("prisma_engine.hip", "prisma_engine_mem.hip"):
+    for f in ("prisma_engine.hip", "prisma_engine_lite.hip", "prisma_engine_mem.hip"):
         o = os.path.join(os.path.dirname(LIB), f + ".timing.o")
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC",
                                "-std=c++17", "-DPRISMA_TIMING=1", "-c", "-o", o,
@@ -42,7 +42,9 @@ topo = Topology.example(topo_name)
 eng = PrismaEngine(topo, engine_params(topo, sim_time_s=60.0, ping_as_obs=PAO, auto_reset=1,
                                       log_capacity=65536 if topo.n_links > 256 else 8192), R)
 lib = load_library()
-timing = lib.prisma_debug_timing_mem if eng.engine_kind == 2 else lib.prisma_debug_timing
+# the kernels without the --train / notify_dest paths live in their own translation unit
+timing = lib.prisma_debug_timing_mem if eng.engine_kind == 2 else (
+    lib.prisma_debug_timing if ", true>" in eng.kernel_name else lib.prisma_debug_timing_lite)
 timing.argtypes = [C.c_void_p]
 if POLICY == "dqn_buffer":
     table = StackedQNet(topo, "buffer", seed=1234, device="cuda").pack()
