@@ -39,7 +39,7 @@
 #include "step_kernel.h"
 
 // memory-resident engine kernels (prisma_engine_mem.hip): 0 step, 1 reset, 2 step + DQN-buffer MLP
-const void* prisma_mem_kernel(int which);
+const void* prisma_mem_kernel(int which, bool ctrl);
 
 
 // mode 0: (re)build every replica at episode P.episode.
@@ -746,9 +746,10 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
         return set_err(PRISMA_ERR_DEVICE, "device initialisation failed");
     }
     if (L.mem) {
-        e->k_step = prisma_mem_kernel(0);
-        e->k_reset = prisma_mem_kernel(1);
-        e->k_step_mlp = prisma_mem_kernel(2);
+        const bool ctrl = L.train || L.notify_dest;
+        e->k_step = prisma_mem_kernel(0, ctrl);
+        e->k_reset = prisma_mem_kernel(1, ctrl);
+        e->k_step_mlp = prisma_mem_kernel(2, ctrl);
     } else {
         // the --train echo and notify_dest paths are compiled only into the instances that need them
         const bool ctrl = L.train || L.notify_dest;

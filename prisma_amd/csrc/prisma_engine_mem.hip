@@ -457,7 +457,7 @@ __global__ void __launch_bounds__(64) prisma_mem_reset_kernel(KParams P) {
     mem_stage(lds, P, r, lane, true);
 }
 
-template <bool MLP>
+template <bool MLP, bool CTRL>
 __global__ void __launch_bounds__(64) prisma_mem_step_kernel(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
@@ -470,6 +470,7 @@ __global__ void __launch_bounds__(64) prisma_mem_step_kernel(KParams P) {
     mem_bind(S, R, P, lv, lds, r, lane);
     S.mlp = P.mlp;
     S.mlp_rp = P.mlp_rp;
+    S.ctrl = CTRL;
 #ifndef PRISMA_MLP_B_MEM
 #define PRISMA_MLP_B_MEM kMlpAll
 #endif
@@ -477,11 +478,13 @@ __global__ void __launch_bounds__(64) prisma_mem_step_kernel(KParams P) {
     mem_stage(lds, P, r, lane, true);
 }
 
-// which: 0 step (table / external), 1 reset, 2 step with the DQN-buffer policy
-const void* prisma_mem_kernel(int which) {
+// which: 0 step (table / external), 1 reset, 2 step with the DQN-buffer policy; ctrl: the
+// --train echo / notify_dest paths compiled in (step_kernel.h)
+const void* prisma_mem_kernel(int which, bool ctrl) {
     if (which == 1) return (const void*)prisma_mem_reset_kernel;
-    if (which == 2) return (const void*)prisma_mem_step_kernel<true>;
-    return (const void*)prisma_mem_step_kernel<false>;
+    if (which == 2) return ctrl ? (const void*)prisma_mem_step_kernel<true, true>
+                                : (const void*)prisma_mem_step_kernel<true, false>;
+    return ctrl ? (const void*)prisma_mem_step_kernel<false, true> : (const void*)prisma_mem_step_kernel<false, false>;
 }
 
 #if PRISMA_TRACE
