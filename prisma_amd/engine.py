@@ -206,19 +206,18 @@ class PrismaEngine:
         sb, lb = C.c_uint32(), C.c_uint32()
         _check(L.prisma_state_bytes(self.h, C.byref(sb), C.byref(lb)))
         self.state_bytes, self.lds_bytes = int(sb.value), int(lb.value)
-        # step-kernel instance the library picked (demangled name prefix, for profiles)
-        self.engine_kind = plan(topo, params)["engine"]
+        # step-kernel instance the library picked (demangled name, for profiles): the register
+        # slots come from prisma_plan; the last template argument says whether the --train echo /
+        # notify_dest paths are compiled in (step_kernel.h)
+        pl = plan(topo, params)
+        self.engine_kind = pl["engine"]
+        ctrl = "true" if (params.get("train") or params.get("notify_dest")) else "false"
         if self.engine_kind == PRISMA_ENGINE_MEMORY:
-            self.kernel_name = "prisma_mem_step_kernel<false>"
-            self.kernel_name_mlp = "prisma_mem_step_kernel<true>"
+            self.kernel_name = f"prisma_mem_step_kernel<false, {ctrl}>"
+            self.kernel_name_mlp = f"prisma_mem_step_kernel<true, {ctrl}>"
         else:
-            fs, ls = 1, 1                  # register slots per lane (64 flows / links each)
-            while 64 * fs < topo.n_flows:
-                fs *= 2
-            while 64 * ls < max(topo.n_links + topo.n_nodes, topo.n_tunnels):
-                ls *= 2
+            fs, ls = pl["flow_slots"], pl["link_slots"]
             tun = "false" if topo.identity else "true"
-            ctrl = "true" if (params.get("train") or params.get("notify_dest")) else "false"
             # template arguments: slots, in-kernel MLP, tunnels, --train/notify_dest paths
             self.kernel_name = f"prisma_step_kernel_t<{fs}, {ls}, false, {tun}, {ctrl}>"
             self.kernel_name_mlp = f"prisma_step_kernel_t<{fs}, {ls}, true, {tun}, {ctrl}>"
