@@ -131,7 +131,7 @@ struct Layout {
     uint32_t PLEN;               // responder positions per tunnel (max tunnel length)
     uint32_t ring_total;         // packet slots over all link FIFOs
     uint32_t lds_state_bytes;    // LDS part of the image (bytes [0, lds_state_bytes))
-    uint32_t s_regs;             // register part: 4 x [64*FS] + 19 x [64*LS] u32 arrays
+    uint32_t s_regs;             // register part: 4 x [64*FS] + 16 x [64*LS] u32 arrays
     uint32_t PBK;                // ping-back delay slots per (tunnel, position) (power of two)
     int32_t  FS, LS;             // flow / link register slots per lane
     // link constants (identical on every switch link: sim.cc:414-433)

@@ -686,7 +686,7 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.s_pbd = take(4u * (uint32_t)(OP.tunnels ? OP.n_resp : OP.T) * L.PBK);
     L.lds_state_bytes = o;
     if (OP.tunnels) L.s_ring = take(4u * tot);      // HBM part of the image
-    L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 19u * 64u * (uint32_t)ls));
+    L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 16u * 64u * (uint32_t)ls));
     L.state_bytes = o;
     // Replicas per CU are bounded by LDS (160 KiB / bytes per replica) for the larger
     // topologies, and a launch whose replicas do not all fit at once runs in rounds
