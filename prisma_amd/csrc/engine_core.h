@@ -461,14 +461,19 @@ __device__ __forceinline__ LinkV link_get(const Regs<FS, LS>& R, uint32_t l) {
 
 // write back a link's fields and recompute its candidate key (registers only:
 // the wire head's key is cached in wh_t / wh_seq)
-template <int FS, int LS>
+// fields a link write-back stores: all, or (wire_pop) only the head, wire count and head key --
+// the readlanes of the fields it leaves alone are then dead code
+constexpr unsigned LP_ALL = 0u, LP_WIRE = 1u;
+template <unsigned MASK = LP_ALL, int FS, int LS>
 __device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, const Hot& H, uint32_t l, const LinkV& k) {
     R.p0.set(l, k.head | (k.txp << 16));
     R.p1.set(l, k.tail | (k.n_wire << 16));
-    R.p2.set(l, k.n_queue | (k.busy << 16));
-    R.qb.set(l, k.qb);
-    R.cp_t.set(l, k.cp_t);
-    R.cp_seq.set(l, k.cp_seq);
+    if (MASK == LP_ALL) {
+        R.p2.set(l, k.n_queue | (k.busy << 16));
+        R.qb.set(l, k.qb);
+        R.cp_t.set(l, k.cp_t);
+        R.cp_seq.set(l, k.cp_seq);
+    }
     R.wh_t.set(l, k.wh_t);
     R.wh_seq.set(l, k.wh_seq);
 }
@@ -1226,7 +1231,7 @@ __device__ __forceinline__ void wire_pop(const Sim& S, RS& R, const Hot& H, uint
         const uint32_t w = k.head & (uint32_t)(L.WCAP() - 1);
         wire_get(S, k, l, w, k.wh_t, k.wh_seq);
     }
-    link_put(S, R, H, l, k);
+    link_put<LP_WIRE>(S, R, H, l, k);
 }
 
 struct Decision {

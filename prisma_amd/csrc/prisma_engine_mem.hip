@@ -197,6 +197,7 @@ __device__ __forceinline__ LinkV link_get(const MemSt& R, uint32_t l) {
     return k;
 }
 
+template <unsigned MASK = LP_ALL>                 // (the whole record is written back either way)
 __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, uint32_t l, const LinkV& k) {
     const uint32_t j = threadIdx.x;
     uint32_t w = k.rec;
