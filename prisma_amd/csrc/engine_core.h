@@ -30,6 +30,7 @@ using namespace prisma;
 #define PRISMA_ABLATE 0
 #endif
 
+
 // instruction-count experiments (A/B builds)
 
 // Diagnostic timing build (-DPRISMA_TIMING=1, scripts/timing.py): s_memtime
@@ -355,12 +356,13 @@ __device__ __forceinline__ void st_rep(const Sim& S, T* p, T v) {
     if (S.mem || S.lane == 0) *p = v;
 }
 
-// A FIFO entry.  Identity overlays of the register-resident engine keep the rings in LDS
-// (lane 0 writes); tunnelled overlays and the memory-resident engine keep them in the HBM
-// state image, written by every lane like st_rep (their arrivals read the packet from
-// the wire slot, so only a dequeue behind a busy transmitter reads the ring back).
+// A FIFO entry, written by every lane (same address, same value).  Identity overlays of the
+// register-resident engine keep the rings in LDS, where an all-lane store needs no exec-mask
+// juggling (A/B +1 % against lane 0 only); tunnelled overlays and the memory-resident engine
+// keep them in the HBM state image (their arrivals read the packet from the wire slot, so only
+// a dequeue behind a busy transmitter reads the ring back).
 __device__ __forceinline__ void ring_put(const Sim& S, uint32_t i, uint32_t e) {
-    if (S.mem || S.tun || S.lane == 0) S.ring[i] = e;
+    S.ring[i] = e;
 }
 
 // uniform LDS reads (every lane reads the same address: broadcast, no conflict)
@@ -591,8 +593,8 @@ __device__ __forceinline__ void wire_set(const Sim& S, LinkV& k, uint32_t l, uin
     if (S.mem) {
         const uint32_t j = (uint32_t)S.lane;
         k.rec = j == LR_WT + i ? t : (j == LR_WT + W + i ? s : (j == LR_WT + 2u * W + i ? x : k.rec));
-    } else if (S.lane == 0) {
-        S.wt[l * W + i] = t;
+    } else {                                  // every lane stores the same value to the same address:
+        S.wt[l * W + i] = t;                  // no exec-mask juggling (A/B +1 % against lane 0 only)
         S.wseq[l * W + i] = s;
         if (S.tun) S.went[l * W + i] = x;
     }
@@ -789,17 +791,15 @@ __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_
     const int lane = S.lane;
     uint64_t rb = __double_as_longlong(reward);
     uint32_t w7 = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | (ttl << 16) | ((H.episode & 0xffu) << 24);
-    uint32_t hw;
-    switch (lane) {
-    case 0: hw = lo32(H.now); break;
-    case 1: hw = hi32(H.now); break;
-    case 2: hw = uid; break;
-    case 3: hw = (uint32_t)prev; break;
-    case 4: hw = (uint32_t)rb; break;
-    case 5: hw = (uint32_t)(rb >> 32); break;
-    case 6: hw = node | (dst << 8) | (start << 16); break;
-    default: hw = w7; break;
-    }
+    // lane l < 8 picks header word l with three lane-bit selects, no per-lane compares
+    // (A/B +3.5 % at the headline against a switch on the lane id)
+    const uint32_t a01 = (lane & 1) ? hi32(H.now) : lo32(H.now);
+    const uint32_t a23 = (lane & 1) ? (uint32_t)prev : uid;
+    const uint32_t a45 = (lane & 1) ? (uint32_t)(rb >> 32) : (uint32_t)rb;
+    const uint32_t a67 = (lane & 1) ? w7 : (node | (dst << 8) | (start << 16));
+    const uint32_t a03 = (lane & 2) ? a23 : a01;
+    const uint32_t a47 = (lane & 2) ? a67 : a45;
+    const uint32_t hw = (lane & 4) ? a47 : a03;
     uint32_t ob = bperm(obs_reg, (uint32_t)(lane - 8) & 63u);
     uint32_t word = lane < 8 ? hw : ob;
     uint32_t* p = (uint32_t*)(S.logrep + (size_t)(d & (S.lv.log_cap() - 1)) * S.lv.rec_bytes());
