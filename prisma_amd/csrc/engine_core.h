@@ -348,12 +348,12 @@ __device__ __forceinline__ int32_t t_fsrc(const Sim& S, uint32_t f) { return S.m
 __device__ __forceinline__ int32_t t_fdst(const Sim& S, uint32_t f) { return S.mem ? S.m_fdst[f] : S.T->fdst[f]; }
 __device__ __forceinline__ double t_fmean(const Sim& S, uint32_t f) { return S.mem ? S.m_fmean[f] : S.T->fmean[f]; }
 
-// A store to replica state that every lane may read back: LDS (register-resident
-// engine) is written by lane 0; HBM (memory-resident engine) by every lane, so each
-// lane's later read of the address is ordered after its own store.
+// A store to replica state that every lane may read back, by every lane (same address, same
+// value): no exec-mask juggling in LDS, and in HBM each lane's later read of the address is
+// ordered after its own store.
 template <class T>
 __device__ __forceinline__ void st_rep(const Sim& S, T* p, T v) {
-    if (S.mem || S.lane == 0) *p = v;
+    *p = v;
 }
 
 // A FIFO entry, written by every lane (same address, same value).  Identity overlays of the

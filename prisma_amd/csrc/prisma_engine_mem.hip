@@ -74,7 +74,7 @@ __device__ __forceinline__ Key lds_key(const uint4* p) {
     return k;
 }
 __device__ __forceinline__ void lds_put_key(const Sim& S, uint4* p, const Key& k) {
-    if (S.lane == 0) *p = make_uint4(lo32(k.t), hi32(k.t), k.s, k.c);
+    *p = make_uint4(lo32(k.t), hi32(k.t), k.s, k.c);     // every lane: same address, same value
 }
 
 // minimum of leaf block b (64 leaves, one per lane): links from LDS, flows from HBM
@@ -143,10 +143,8 @@ __device__ __forceinline__ Key block_min_cached(const Sim& S, const MemSt& R, ui
 __device__ __forceinline__ void tree_touch(const Sim& S, MemSt& R, const Hot& H, uint32_t leaf, int64_t t,
                                            uint32_t seq, uint32_t code, uint32_t aux) {
     if (leaf < R.L) {
-        if (S.lane == 0) {
-            R.lkey[leaf] = make_uint2(lo32(t), seq);
-            R.lkind[leaf] = (uint8_t)aux;
-        }
+        R.lkey[leaf] = make_uint2(lo32(t), seq);              // every lane: same address, same value
+        R.lkind[leaf] = (uint8_t)aux;
     } else {
         st_rep(S, &R.fkeys[leaf - R.L], make_uint4(lo32(t), hi32(t), seq, aux));
     }
