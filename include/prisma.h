@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PRISMA_ABI_VERSION 6
+#define PRISMA_ABI_VERSION 7
 
 /* status codes */
 #define PRISMA_OK              0
@@ -76,7 +76,15 @@ extern "C" {
                                       256 links / tunnels, 512 flows             */
 #define PRISMA_ENGINE_MEMORY   2   /* replica state in HBM under an event tree:
                                       <= 256 nodes, links + flows <= 262 144,
-                                      identity overlays (ER-256)                 */
+                                      identity overlays (ER-256), signalling type
+                                      "ideal" without big signalling              */
+
+/* signalling type (prisma_params_t.signaling_type, argument_parser.py:72 /
+   sim.cc:142, 373-392): the payload of the --train small-signalling echo a node
+   sends, 0 B ("ideal"), 8 + 8 (overlay degree + 1) B ("NN") or 24 B ("target") */
+#define PRISMA_SIGNALING_IDEAL  0
+#define PRISMA_SIGNALING_NN     1
+#define PRISMA_SIGNALING_TARGET 2
 
 /* per-decision status (prisma_record_t.status) */
 #define PRISMA_ST_PENDING      0   /* waiting for an action (prisma_step)  */
@@ -151,14 +159,29 @@ typedef struct prisma_params {
                                    made while one packet crosses one link) */
     uint32_t notify_dest;       /* prisma_step also stops at arrivals at the
                                    destination (done=True notifications) and
-                                   at small-signalling arrivals (control:
-                                   obs [1000, signalled uid]); the action
-                                   given for them is ignored               */
+                                   at control arrivals, obs [1000, a, b, c]:
+                                   small-signalling echo: a = signalled uid,
+                                   b = its size on the wire, c = 0; big
+                                   signalling: a = NN index, b = segment
+                                   index, c = 0x10000 | overlay index of the
+                                   signalling node; the action given for
+                                   them is ignored                          */
     uint32_t train;             /* --train: every data notification at a
-                                   non-source node echoes a 30-B small-
-                                   signalling packet to its last hop
+                                   non-source node echoes a small-signalling
+                                   packet to its last hop
                                    (data-packet-manager.cc:301-347)        */
     uint32_t engine;            /* PRISMA_ENGINE_* (0 = auto)              */
+    /* ---- ABI 7 ---- */
+    uint32_t signaling_type;    /* PRISMA_SIGNALING_*          ["ideal"]   */
+    uint32_t big_signaling;     /* --signaling (signalingSim) with "NN" and
+                                   --train: per flow between overlay
+                                   neighbours, a BigSignalingGenerator-
+                                   Application sending 512-B NN-weight
+                                   segments to the neighbour from AppStartTime
+                                   on (sim.cc:634-647, big-signaling-
+                                   application.cc:224-309)                 */
+    float    sync_step_s;       /* syncStep: seconds per NN copy   [1.0]   */
+    uint32_t big_signaling_bytes; /* bigSignalingSize: NN bytes   [35328]  */
 } prisma_params_t;
 
 /*

@@ -38,6 +38,8 @@ class OrConfig(C.Structure):
         ("overlay_nodes", C.POINTER(C.c_int32)), ("overlay_index", C.POINTER(C.c_int32)),
         ("ov_row_ptr", C.POINTER(C.c_int32)), ("tun_dst", C.POINTER(C.c_int32)),
         ("tun_link", C.POINTER(C.c_int32)), ("next_link", C.POINTER(C.c_int32)),
+        ("signaling_type", C.c_uint32), ("big_signaling", C.c_uint32), ("sync_step_s", C.c_float),
+        ("big_signaling_bytes", C.c_uint32),
     ]
 
 
@@ -161,6 +163,10 @@ class OracleSim:
                 if x != y:
                     nl[x, y] = topo.link_id(x, int(topo.next_hop[x, y]))
         cfg.next_link = arr(nl, C.c_int32, np.int32)
+        cfg.signaling_type = int(params.get("signaling_type", 0))
+        cfg.big_signaling = int(params.get("big_signaling", 0))
+        cfg.sync_step_s = float(params.get("sync_step_s", 1.0))
+        cfg.big_signaling_bytes = int(params.get("big_signaling_bytes", 35328))
         self._cfg = cfg
         self.W = topo.obs_width
         self.rec_dtype = record_dtype(self.W)

@@ -127,8 +127,8 @@ typedef struct {
 } counters_t;
 
 enum { ST_PENDING = 0, ST_ENQUEUED = 1, ST_DROPPED = 2, ST_DEST = 3, ST_DISCARDED = 4 };
-enum { DATA_PACKET = 0, SMALL_SIGN_PACKET = 2, PING_FORWARD_PACKET = 3, PING_BACK_PACKET = 4 };   /* enum-and-constants.h:5-11 */
-enum { EV_PING = 0, EV_START = 1, EV_SEND = 2, EV_COMPLETE = 3, EV_RECEIVE = 4 };
+enum { DATA_PACKET = 0, BIG_SIGN_PACKET = 1, SMALL_SIGN_PACKET = 2, PING_FORWARD_PACKET = 3, PING_BACK_PACKET = 4 };   /* enum-and-constants.h:5-11 */
+enum { EV_PING = 0, EV_START = 1, EV_SEND = 2, EV_COMPLETE = 3, EV_RECEIVE = 4, EV_BSTART = 5, EV_BSEND = 6 };
 
 /* ------------------------------------------------------------------ */
 /* simulation objects                                                  */
@@ -137,7 +137,7 @@ typedef struct {              /* MyTag (my-tag.h:49-65) + size */
     int type, src, dst, next_hop, last_hop;
     uint64_t start_time;      /* data: whole seconds; ping: ms          */
     int valable;
-    uint32_t uid, ping_idx;
+    uint32_t uid, ping_idx;   /* big signalling: ping_idx = send index n of its generator */
     int tunnel;               /* ping: the origin's local tunnel index      */
     int ttl;                  /* IP TTL (data: 255 at the app, :330)       */
     float one_hop_delay;
@@ -183,6 +183,11 @@ struct or_sim {
     sentvec_t* unacked;         /* per tunnel (node, local index)        */
     fvec_t* delays;
     uvec_t* lost;               /* per node m_lostPackets (uids)         */
+    uint32_t* echo_payload;     /* per node: small-signalling payload (sim.cc:373-392) */
+    int G;                      /* big-signalling generators (sim.cc:634-647), flow order */
+    int *g_src, *g_dst, *g_draws;
+    int64_t bs_period;          /* ScheduleNextTx delay (big-signaling-application.cc:247-250) */
+    uint32_t bs_nseg;           /* segments per NN copy: m_pktSizeMean / m_segSize      */
     temp_t* temp; int64_t temp_cap;
     uint32_t next_uid;
     counters_t cnt;
@@ -475,6 +480,36 @@ static void build_ctrl_info(or_sim_t* s, const pkt_t* k, int v) {
     snprintf(b + n, cap - n, ", PacketIdSignaled=%u, Arrived at final dest=%d", k->uid, (int)(k->dst == v));
 }
 
+static void bsig_index(const or_sim_t* s, uint32_t n, uint32_t* nn, uint32_t* seg);
+
+/* big-signalling info: PacketManager::getInfo (tokens 0-17) + BigSignalingPacketManager::getInfo
+ * (big-signaling-packet-manager.cc:111-123).  Token 3 (the segment's ns-3 packet uid) is not
+ * modelled: 0; the start-time tag is never set, so token 0 is the current time. */
+static void build_big_info(or_sim_t* s, const pkt_t* k, int v) {
+    char* b = s->info;
+    size_t cap = sizeof(s->info), n = 0;
+    double now = get_seconds(s->now);
+    float avg_e2e = s->cnt.e2e_n ? s->cnt.e2e_sum / (float)s->cnt.e2e_n : 0.0f;
+    float avg_cost = s->cnt.cost_n ? s->cnt.cost_sum / (float)s->cnt.cost_n : 0.0f;
+    float sig = s->cnt.bytes_data ? (float)s->cnt.bytes_signaling / (float)s->cnt.bytes_data : 0.0f;
+    uint32_t nn, seg;
+    bsig_index(s, k->ping_idx, &nn, &seg);
+    (void)v;
+    n += snprintf(b + n, cap - n, "End to End Delay=%f, Packet Size=%u, Current sim time =%f, Pkt ID =%u, packetType =%d",
+                  now - (double)k->start_time, k->size, now, k->uid, k->type);
+    n += snprintf(b + n, cap - n, ", Avg End to End Delay =%f, Avg Cost =%f, Avg Underlay End to End Delay =%f, Avg Underlay Cost =%f",
+                  (double)avg_e2e, (double)avg_cost, 0.0, 0.0);
+    n += snprintf(b + n, cap - n, ", Packets dropped =%d, Packets delivered =%d, Packets injected =%d,Packets Buffered =%d",
+                  s->cnt.ov_lost, s->cnt.ov_arrived, s->cnt.ov_injected,
+                  s->cnt.ov_injected - (s->cnt.ov_arrived + s->cnt.ov_lost));
+    n += snprintf(b + n, cap - n, ", Packets dropped Underlay =%d, Packets delivered Underlay=%d, Packets injected Underlay=%d,Packets Buffered Underlay=%d",
+                  s->cnt.un_lost, s->cnt.un_arrived, s->cnt.un_injected,
+                  s->cnt.un_injected - (s->cnt.un_arrived + s->cnt.un_lost));
+    n += snprintf(b + n, cap - n, ",Signaling overhead =%f", (double)sig);
+    snprintf(b + n, cap - n, ", NN Index=%u, segment Index=%u, NodeId Signaled=%d", nn, seg,
+             s->c.overlay_index[k->src]);
+}
+
 /* ------------------------------------------------------------------ */
 /* event handlers                                                      */
 /* ------------------------------------------------------------------ */
@@ -572,8 +607,36 @@ static void send_small_signaling(or_sim_t* s, const pkt_t* data, int v, int l_in
     e->start_time = 0;
     e->valable = 0;
     e->ttl = 64;
-    e->size = 0 + 8 + 20 + 2;
+    e->size = s->echo_payload[v] + 8 + 20 + 2;          /* m_signPacketSize (sim.cc:373-392) */
     dev_send(s, s->c.link_rev[l_in], q);               /* m_receivingNetDev->Send */
+}
+
+/* BigSignalingGeneratorApplication (big-signaling-application.cc:224-309): StartSending at
+ * AppStartTime schedules the first SendPacket one period later; every SendPacket hands a
+ * 512-B segment (tag: type 1, source/nextHop/destination, lastHop 1000, segment and NN index)
+ * to the UDP socket of the traffic node -- its access link -- and schedules the next. */
+static void bsig_send_packet(or_sim_t* s, int g) {
+    uint32_t n = (uint32_t)++s->g_draws[g];                         /* ScheduleNextTx counted it */
+    int p = pkt_alloc(s);
+    pkt_t* k = &s->pk[p];
+    k->type = BIG_SIGN_PACKET;
+    k->src = s->g_src[g];
+    k->dst = k->next_hop = s->g_dst[g];
+    k->last_hop = 1000;
+    k->start_time = 0;
+    k->valable = 0;
+    k->uid = 0;                                                       /* ns-3 packet uid: not modelled */
+    k->ping_idx = n;
+    k->ttl = 255;                                                     /* SetIpTtl(255) :282 */
+    k->size = 512 + 8 + 20 + 2;
+    dev_send(s, s->E + s->g_src[g], p);
+    schedule(s, s->now + s->bs_period, EV_BSEND, g, -1);
+}
+/* segment / NN index of the n-th segment (ScheduleNextTx :241-246: the index is bumped
+ * before each send and wraps to 0 -- next NN copy -- at m_pktSizeMean / m_segSize) */
+static void bsig_index(const or_sim_t* s, uint32_t n, uint32_t* nn, uint32_t* seg) {
+    if (s->bs_nseg <= 1) { *nn = n; *seg = 0; return; }
+    *nn = n / s->bs_nseg; *seg = n % s->bs_nseg;
 }
 
 static void flow_schedule_next(or_sim_t* s, int f) {                /* poisson-application.cc:265-295 */
@@ -730,7 +793,17 @@ static int receive(or_sim_t* s, int di, int p) {
         s->pend = 1; s->pend_pkt = p; s->pend_node = v; s->pend_link = di; s->pend_rec = dn;
         return 1;
     }
-    if (k->type == SMALL_SIGN_PACKET) {
+    if (k->type == BIG_SIGN_PACKET) {
+        /* BigSignalingPacketManager::receivePacket (big-signaling-packet-manager.cc:93-108):
+         * not at the packet's source; valid (nextHop == node, at its final destination) -> Notify */
+        if (overlay && k->src != v && k->next_hop == v && k->dst == v) {
+            build_big_info(s, k, v);
+            if (s->c.notify_dest) {
+                s->pend = 1; s->pend_ctrl = 1; s->pend_pkt = p; s->pend_node = v; s->pend_link = di;
+                return 1;
+            }
+        }
+    } else if (k->type == SMALL_SIGN_PACKET) {
         /* SmallSignalingPacketManager::receivePacket (small-signaling-packet-manager.cc:86-94):
          * valid (nextHop == node and arrived at its final destination) -> Notify */
         if (k->next_hop == v && k->dst == v) {
@@ -767,6 +840,8 @@ static int run_until_decision(or_sim_t* s) {
         case EV_PING: send_ping_packets(s, e.id); break;
         case EV_START: flow_schedule_next(s, e.id); break;             /* StartSending -> ScheduleNextTx */
         case EV_SEND: flow_send_packet(s, e.id); break;
+        case EV_BSTART: schedule(s, s->now + s->bs_period, EV_BSEND, e.id, -1); break;   /* StartSending */
+        case EV_BSEND: bsig_send_packet(s, e.id); break;
         case EV_COMPLETE: transmit_complete(s, e.id); break;
         case EV_RECEIVE:
             if (receive(s, e.id, e.pkt)) return 1;
@@ -812,6 +887,33 @@ or_sim_t* or_create(const or_config_t* cfg) {
     s->delays = calloc((size_t)cfg->n_tunnels + 1, sizeof(fvec_t));
     s->lost = calloc((size_t)s->N, sizeof(uvec_t));
     s->cnt.episode = cfg->episode;
+    /* signalling (sim.cc:373-392): echo payload by the overlay degree of its sender */
+    s->echo_payload = calloc((size_t)s->N, sizeof(uint32_t));
+    for (int u = 0; u < s->N; ++u) {
+        uint32_t odeg = (uint32_t)(cfg->ov_row_ptr[u + 1] - cfg->ov_row_ptr[u]);
+        s->echo_payload[u] = cfg->signaling_type == 1 ? 8u + 8u * (odeg + 1u) : (cfg->signaling_type == 2 ? 24u : 0u);
+    }
+    /* big signalling (sim.cc:634-647): inside the flow loop, one generator per flow between
+     * overlay neighbours; ScheduleNextTx's period in the reference's own arithmetic: the
+     * uint32 size * 8 over the float syncStep is a float, 4096 over that a double */
+    s->g_src = calloc((size_t)s->F + 1, sizeof(int));
+    s->g_dst = calloc((size_t)s->F + 1, sizeof(int));
+    s->g_draws = calloc((size_t)s->F + 1, sizeof(int));
+    int* g_of_flow = calloc((size_t)s->F + 1, sizeof(int));
+    const int bsig = cfg->train && cfg->big_signaling && cfg->signaling_type == 1;
+    for (int f = 0; f < s->F; ++f) {
+        g_of_flow[f] = -1;
+        if (!bsig) continue;
+        const int u = cfg->flow_src[f], w = cfg->flow_dst[f];
+        for (int t = cfg->ov_row_ptr[u]; t < cfg->ov_row_ptr[u + 1]; ++t)
+            if (cfg->tun_dst[t] == w) { g_of_flow[f] = s->G; s->g_src[s->G] = u; s->g_dst[s->G] = w; s->G++; break; }
+    }
+    {
+        const float rate = (float)(cfg->big_signaling_bytes * 8u) / cfg->sync_step_s;
+        const double delay = (double)(512u * 8u) / (double)rate;
+        s->bs_period = or_seconds_to_ns(delay);
+        s->bs_nseg = cfg->big_signaling_bytes / 512u;
+    }
     /* setup-time schedule: ping timers (sim.cc:544 -> data-packet-manager.cc:118-121)
        in overlay order, then application starts (Node::Initialize at t=0) in
        flow (src, dst) order (sim.cc:599-631) */
@@ -824,7 +926,9 @@ or_sim_t* or_create(const or_config_t* cfg) {
         uint64_t u53 = ((uint64_t)(x[0] >> 5) << 26) | (uint64_t)(x[1] >> 6);
         double U = (double)u53 * (1.0 / 9007199254740992.0);
         schedule(s, or_seconds_to_ns(0.0001 + U), EV_START, f, -1);
+        if (g_of_flow[f] >= 0) schedule(s, or_seconds_to_ns(0.0001), EV_BSTART, g_of_flow[f], -1);   /* AppStartTime */
     }
+    free(g_of_flow);
     return s;
 }
 
@@ -835,6 +939,7 @@ void or_destroy(or_sim_t* s) {
     for (int u = 0; u < s->N; ++u) free(s->lost[u].a);
     free(s->dev); free(s->flow_draws); free(s->flow_mean); free(s->ping_index);
     free(s->unacked); free(s->delays); free(s->lost); free(s->temp);
+    free(s->echo_payload); free(s->g_src); free(s->g_dst); free(s->g_draws);
     free(s->heap); free(s->pk); free(s->rec); free(s->tr);
     free(s);
 }
@@ -843,9 +948,19 @@ int or_step(or_sim_t* s, int32_t action, int32_t* obs_out) {
     if (s->pend) finish_data_decision(s, action);
     int r = run_until_decision(s);
     if (r && obs_out && s->pend_ctrl) {             /* GetObservation for a control packet: [1000] */
+        const pkt_t* k = &s->pk[s->pend_pkt];
         for (int i = 0; i < s->W; ++i) obs_out[i] = 0;
-        obs_out[0] = 1000;
-        obs_out[1] = (int32_t)s->pk[s->pend_pkt].uid;  /* the signalled uid (engine ABI: obs[1]) */
+        obs_out[0] = 1000;                          /* + the info fields (engine ABI: include/prisma.h) */
+        if (k->type == BIG_SIGN_PACKET) {
+            uint32_t nn, seg;
+            bsig_index(s, k->ping_idx, &nn, &seg);
+            obs_out[1] = (int32_t)nn;
+            obs_out[2] = (int32_t)seg;
+            obs_out[3] = 0x10000 | s->c.overlay_index[k->src];
+        } else {
+            obs_out[1] = (int32_t)k->uid;           /* the signalled uid */
+            obs_out[2] = (int32_t)k->size;
+        }
         return r;
     }
     if (r && obs_out) {

@@ -59,6 +59,11 @@ typedef struct or_config {
     const int32_t* tun_link;        /* [n_tunnels] first physical link       */
     const int32_t* next_link;       /* [n_nodes * n_nodes] link x -> towards y
                                        (ns-3 global routing, -1 if x == y)   */
+    /* signalling (sim.cc:142-144, 373-392, 634-647) */
+    uint32_t signaling_type;    /* 0 "ideal", 1 "NN", 2 "target": echo payload */
+    uint32_t big_signaling;     /* --signaling: NN-weight generators (with NN and train) */
+    float    sync_step_s;       /* syncStep                                  */
+    uint32_t big_signaling_bytes; /* bigSignalingSize                        */
 } or_config_t;
 
 typedef struct or_sim or_sim_t;

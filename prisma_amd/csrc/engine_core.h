@@ -415,7 +415,15 @@ __device__ __forceinline__ bool key_less(int64_t t, uint32_t s, int64_t bt, uint
     return t < bt || (t == bt && s < bs);
 }
 
-__device__ __forceinline__ uint32_t ent_size(const LV& L, uint32_t x) {
+// size on the wire of entry x on link l.  The --train instances read an echo's size per
+// link (its sender's payload with signalling type "NN" or "target", sim.cc:373-392) and
+// know the big-signalling segment; the other instances never see either.
+__device__ __forceinline__ uint32_t ent_size(const Sim& S, uint32_t x, uint32_t l) {
+    const LV& L = S.lv;
+    if (S.ctrl && !S.mem) {
+        if (ent_is_echo(x)) return S.T->esz[l];
+        if (ent_is_big(x)) return S.T->bs_size;
+    }
     return ent_is_data(x) ? L.data_size() : (ent_is_echo(x) ? L.echo_size() : L.ping_size());
 }
 // whole seconds of a (non-negative) time: unsigned division by a constant is shorter
@@ -620,9 +628,11 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
     const LV& L = S.lv;
     const bool sw = l < (uint32_t)L.E();
     // register-resident engine: a switch link's tx time by entry class from the topology image
+    // (--train instances: an echo's by link, sized by its sender)
     int64_t tx = sw ? (S.mem ? (ent_is_data(x) ? L.sw_txd() : (ent_is_echo(x) ? L.sw_txe() : L.sw_txp()))
-                             : (int64_t)S.T->ctx[ent_cls(x)])
-                    : t_acctx(S, l - (uint32_t)L.E());
+                             : (int64_t)((S.ctrl && ent_is_echo(x)) ? S.T->etx[l] : S.T->ctx[ent_cls(x)]))
+                    : ((S.ctrl && !S.mem && ent_is_big(x)) ? (int64_t)S.T->abtx[l - (uint32_t)L.E()]
+                                                           : t_acctx(S, l - (uint32_t)L.E()));
     int64_t prop = sw ? L.sw_prop() : 0;
     k.busy = 1;
     k.cp_t = lo32(H.now + tx);
@@ -642,7 +652,7 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
 template <class RS>
 __device__ __forceinline__ int link_send_k(const Sim& S, RS& R, Hot& H, uint32_t l, uint32_t e, LinkV k) {
     const LV& L = S.lv;
-    uint32_t size = ent_size(L, e);
+    uint32_t size = ent_size(S, e, l);
     bool ok = l < (uint32_t)L.E() ? (k.qb + size <= L.qmax_bytes()) : (k.n_queue + 1u <= L.acc_qmax_pkts());
     if (!ok) return 0;
     if (RS::kLazy) {
@@ -664,7 +674,7 @@ __device__ __forceinline__ int link_send_k(const Sim& S, RS& R, Hot& H, uint32_t
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
-        k.qb -= ent_size(L, hx);
+        k.qb -= ent_size(S, hx, l);
         transmit_start(S, H, l, k, xi, hx);
     }
     link_put(S, R, H, l, k);
@@ -674,7 +684,7 @@ template <class RS>
 __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l, uint32_t e) {
     const LV& L = S.lv;
     LinkV k = link_get(R, l);
-    uint32_t size = ent_size(L, e);
+    uint32_t size = ent_size(S, e, l);
     bool ok = l < (uint32_t)L.E() ? (k.qb + size <= L.qmax_bytes()) : (k.n_queue + 1u <= L.acc_qmax_pkts());
     if (!ok) return 0;
     if (RS::kLazy) {
@@ -696,7 +706,7 @@ __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
-        k.qb -= ent_size(L, hx);
+        k.qb -= ent_size(S, hx, l);
         transmit_start(S, H, l, k, xi, hx);
     }
     link_put(S, R, H, l, k);
@@ -716,7 +726,7 @@ __device__ __forceinline__ void on_complete(const Sim& S, RS& R, Hot& H, uint32_
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
-        k.qb -= ent_size(L, hx);
+        k.qb -= ent_size(S, hx, l);
         transmit_start(S, H, l, k, xi, hx);
     }
     link_put(S, R, H, l, k);
@@ -821,9 +831,10 @@ __device__ __forceinline__ void patch_status(const Sim& S, uint32_t d, uint32_t 
 
 // Receive tail after the MacRx trace (point-to-point-net-device.cc:430-463).
 // arrived: a data packet at its destination (start = its start second).
+// l: the arrival link (the size of an echo)
 template <class RS>
 __device__ __forceinline__ void receive_counters(const Sim& S, RS& R, const Hot& H, uint32_t x, bool arrived,
-                                                 uint32_t start) {
+                                                 uint32_t start, uint32_t l) {
     const LV& L = S.lv;
     if (arrived) {
         // valable, nextHop == finalDest on identity overlays
@@ -835,7 +846,7 @@ __device__ __forceinline__ void receive_counters(const Sim& S, RS& R, const Hot&
         CNT_ADD(S, e2e_n, 1u);
     }
     // pings are always addressed to the node that receives them
-    if (!ent_is_data(x)) CNT_ADD(S, bytes_signaling, ent_size(L, x) - 2u);
+    if (!ent_is_data(x)) CNT_ADD(S, bytes_signaling, ent_size(S, x, l) - 2u);
     if (ent_type(x) == T_FRESH) {
         CNT_ADD(S, ov_injected, 1u);
         CNT_ADD(S, bytes_data, L.data_size() - 2u);
@@ -909,7 +920,7 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
 #endif
     if (fused) write_record(S, H, d, reward, uid, prev, v, dst, start, action, status, obs_reg, ttl);
     else patch_record(S, H, d, action, status);
-    receive_counters(S, R, H, x, false, 0u);
+    receive_counters(S, R, H, x, false, 0u, 0u);
 #if PRISMA_TIMING
     { const uint64_t t = TM_NOW(); S.tsub[1] += t - S.tlast; S.tlast = t; }
 #endif
@@ -925,14 +936,14 @@ __device__ __forceinline__ int finish_pending(const Sim& S, RS& R, Hot& H, int a
     H.pend = 0;
     const uint32_t x = u_ld32(&h.pend_ent[0]), flags = u_ld32(&h.pend_ent[3]);
     if (S.ctrl && (flags & PEND_CTRL)) {
-        receive_counters(S, R, H, x, false, 0u);
+        receive_counters(S, R, H, x, false, 0u, u_ld32(&h.pend_link));
         return 0;
     }
     const uint32_t echo_link = (S.ctrl && (flags & PEND_ECHO)) ? (uint32_t)t_lrev(S, u_ld32(&h.pend_link)) : kNoLink;
     const uint32_t last = u_ld32(&h.pend_last);
     if (S.ctrl && (flags & PEND_DEST)) {
         if (echo_link != kNoLink) send_echo(S, R, H, echo_link, u_ld32(&h.pend_uid), last);
-        receive_counters(S, R, H, x, true, u_ld32(&h.pend_ent[2]));
+        receive_counters(S, R, H, x, true, u_ld32(&h.pend_ent[2]), 0u);
         return 0;
     }
     apply_decision(S, R, H, x, 0u, 0u, u_ld32(&h.pend_uid), u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action,
@@ -975,6 +986,29 @@ __device__ __forceinline__ void flow_next(const Sim& S, RS& R, Hot& H, uint32_t 
     flow_set(S, R, H, f, t, H.seq++, draw + 1);
 }
 
+// The BigSignalingGeneratorApplications (big-signaling-application.cc:224-309), all in flow
+// slot F.  Every generator starts at AppStartTime and sends one 512-B segment per period, so
+// all of them fire at the same instants, in install order (their seqs were taken in that order
+// one period earlier, and every seq taken in between belongs to an access-link event of the
+// group, at most one transmission later): like a ping round, one slot executes the G
+// consecutive ns-3 events -- the first of them starts the sends (StartSending), the others
+// hand segment k to the traffic node's access link (SendPacket :261-309) -- and re-arms with
+// the seq of the first reschedule (ScheduleNextTx :235-259).
+template <class RS>
+__device__ __forceinline__ void on_bsig(const Sim& S, RS& R, Hot& H, uint32_t f) {
+    const uint32_t k = flow_draw(S, R, f);
+    const uint32_t G = S.T->n_bsig, E = (uint32_t)S.lv.E();
+    if (k > kUidMask) fail(H, PRISMA_EBIT_TIME);                    // 21-bit send index
+    uint32_t first = 0;
+    for (uint32_t g = 0; g < G; ++g) {
+        if (k != 0 && !link_send(S, R, H, E + (S.T->bpair[g] & 255u), g_make(g, k))) CNT_ADD(S, ctrl_dropped, 1u);
+        const uint32_t sq = H.seq++;
+        if (g == 0) first = sq;
+    }
+    H.ev_launch += G - 1u;
+    flow_set(S, R, H, f, H.now + S.T->bs_period, first, k + 1u);
+}
+
 template <class RS>
 __device__ __forceinline__ void on_flow(const Sim& S, RS& R, Hot& H, uint32_t f) {
     // memory-resident engine: the access link's record is fetched first, so its load and the
@@ -990,6 +1024,7 @@ __device__ __forceinline__ void on_flow(const Sim& S, RS& R, Hot& H, uint32_t f)
             H.uid++;
         }
     } else {
+        if (S.ctrl && f >= (uint32_t)S.lv.F()) { on_bsig(S, R, H, f); return; }
         draw = flow_draw(S, R, f);
         if (draw != 0) {
             const uint32_t src = (uint32_t)t_fsrc(S, f);
@@ -1418,13 +1453,34 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
                 return 1;
             }
             if (echo) send_echo(S, R, H, (uint32_t)t_lrev(S, l), uid, last);
-            receive_counters(S, R, H, x, true, start);
+            receive_counters(S, R, H, x, true, start, 0u);
             return 0;
         }
         if (!fused) write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_PENDING, o, ttl);
         return 1;
     }
     wire_pop(S, R, H, l, k);
+    if (S.ctrl && !S.mem && ent_is_big(x)) {                        // (only with --signaling and --train)
+        const uint32_t bp = S.T->bpair[g_gen(x)];
+        const uint32_t src = bp & 255u, dst = (bp >> 8) & 255u;
+        if (v == src) {                  // from the traffic node: IP-forwarded towards its destination
+            if (!link_send(S, R, H, (bp >> 16) & 255u, x)) CNT_ADD(S, ctrl_dropped, 1u);
+            return 0;
+        }
+        if (tun && v != dst) { ctrl_forward(S, R, H, v, dst, x); return 0; }
+        // BigSignalingPacketManager::receivePacket (big-signaling-packet-manager.cc:93-108):
+        // at its destination, not its source -> Notify; obs [1000] (+ NN / segment index, sender)
+        if (!fused && L.notify_dest()) {
+            const uint32_t n = g_n(x), ns = S.T->bs_nseg;
+            const uint32_t nn = ns <= 1u ? n : n / ns, seg = ns <= 1u ? 0u : n % ns;
+            const uint32_t so = 0x10000u | (tun ? (uint32_t)S.T->ovi[src] : src);
+            D.x = x; D.v = v; D.uid = 0u; D.flags = PEND_CTRL; D.last = 0u;
+            D.obs = (S.lane == 0) ? 1000u : ((S.lane == 1) ? nn : ((S.lane == 2) ? seg : ((S.lane == 3) ? so : 0u)));
+            return 1;
+        }
+        receive_counters(S, R, H, x, false, 0u, l);
+        return 0;
+    }
     if (S.ctrl && ent_is_echo(x)) {                                 // (echoes exist only with --train)
         const uint32_t to = e_to(x);
         if (tun && to != v) { ctrl_forward(S, R, H, v, to, x); return 0; }
@@ -1432,10 +1488,11 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         // addressed to this node, so valid -> Notify; the agent sees obs [1000]
         if (!fused && S.ctrl && L.notify_dest()) {
             D.x = x; D.v = v; D.uid = e_uid(x); D.flags = PEND_CTRL; D.last = 0u;
-            D.obs = (S.lane == 0) ? 1000u : ((S.lane == 1) ? e_uid(x) : 0u);
+            const uint32_t sz = ent_size(S, x, l);
+            D.obs = (S.lane == 0) ? 1000u : ((S.lane == 1) ? e_uid(x) : ((S.lane == 2) ? sz : 0u));
             return 1;
         }
-        receive_counters(S, R, H, x, false, 0u);
+        receive_counters(S, R, H, x, false, 0u, l);
         return 0;
     }
     // pings.  NotifyPktRcv hands every ping seen on an overlay node's devices to
@@ -1472,7 +1529,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         }
         if (org != v) { ctrl_forward(S, R, H, v, org, x); return 0; }
     }
-    receive_counters(S, R, H, x, false, 0u);
+    receive_counters(S, R, H, x, false, 0u, l);
     return 0;
 }
 
@@ -1490,6 +1547,10 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
     __syncthreads();
     uint4* st4 = (uint4*)S.base;
     for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes() / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
+    // big-signalling generators: flow slot F (on_bsig), each generator started right after its
+    // flow (sim.cc:599-647: the start events in install order, fseq)
+    const bool bsig = S.ctrl && !S.mem;
+    const uint32_t nbs = bsig ? S.T->n_bsig : 0u;
 #pragma unroll
     for (int j = 0; j < FS; ++j) {
         uint32_t f = (uint32_t)lane + 64u * j;
@@ -1501,7 +1562,10 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
             uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
             double U = (double)u53 * (1.0 / 9007199254740992.0);
             t = sec_to_ns(0.0001 + U);                              // sim.cc:610-630
-            s = (uint32_t)L.NO() + f;                          // after the NO ping timers
+            s = bsig ? S.T->fseq[f] : (uint32_t)L.NO() + f;    // after the NO ping timers
+        } else if (nbs && f == (uint32_t)L.F()) {
+            t = sec_to_ns(0.0001);                                  // AppStartTime (sim.cc:244, 645)
+            s = S.T->fseq[f];                                       // generator 0's start
         }
         R.fk_lo.v[j] = lo32(t); R.fk_hi.v[j] = hi32(t); R.fk_seq.v[j] = s; R.f_draw.v[j] = 0;
     }
@@ -1517,7 +1581,7 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
     H.now = 0;
     H.ping_t = L.ping_period();                                       // data-packet-manager.cc:118-121
     H.ping_seq = 0;
-    H.seq = (uint32_t)L.NO() + (uint32_t)L.F();
+    H.seq = (uint32_t)L.NO() + (uint32_t)L.F() + nbs;
     H.uid = 0; H.ping_rounds = 0; H.pend = 0; H.over = 0; H.error = 0; H.stop = 0;
     H.dec = dec; H.hops_launch = hl; H.ev_launch = el;
     H.episode = episode;

@@ -28,11 +28,20 @@ constexpr uint32_t K_PING = 0u, K_FLOW = 1u, K_COMPLETE = 2u, K_ARRIVE = 3u;
 //   echo     small-signalling packet (--train): T_PBACK with bit 31 set,
 //            bits 2-9 = its destination node (the data packet's last hop),
 //            bits 10-30 = the signalled data packet's uid mod 2^21
+//   big      big-signalling segment (--signaling, "NN"): T_PFWD with bit 31 set,
+//            bits 2-9 = its generator (TopoImage::bpair), bits 10-30 = the
+//            generator's send index (segment and NN index derive from it)
 constexpr uint32_t T_RELAY = 0u, T_FRESH = 1u, T_PFWD = 2u, T_PBACK = 3u;
 constexpr uint32_t kEchoBit = 1u << 31;
 __host__ __device__ inline uint32_t ent_type(uint32_t x) { return x & 3u; }
 __host__ __device__ inline bool ent_is_data(uint32_t x) { return (x & 2u) == 0u; }
 __host__ __device__ inline bool ent_is_echo(uint32_t x) { return (x & (kEchoBit | 3u)) == (kEchoBit | T_PBACK); }
+__host__ __device__ inline bool ent_is_big(uint32_t x) { return (x & (kEchoBit | 3u)) == (kEchoBit | T_PFWD); }
+__host__ __device__ inline uint32_t g_make(uint32_t gen, uint32_t n) {
+    return T_PFWD | kEchoBit | (gen << 2) | ((n & ((1u << 21) - 1u)) << 10);
+}
+__host__ __device__ inline uint32_t g_gen(uint32_t x) { return (x >> 2) & 255u; }
+__host__ __device__ inline uint32_t g_n(uint32_t x) { return (x >> 10) & ((1u << 21) - 1u); }
 __host__ __device__ inline uint32_t r_make(uint32_t dec, uint32_t src) {
     return T_RELAY | ((dec & ((1u << 22) - 1u)) << 2) | (src << 24);
 }
@@ -112,6 +121,18 @@ struct TopoImage {
                                  // position mask << 16 (overlay nodes on the tunnel, target included)
     uint32_t ctx[8];             // transmission time on a switch link of an entry of class
                                  // (type | echo bit << 2), ns (< 2^31)
+    // signalling (read only by the --train instances, step_kernel.h CTRL)
+    uint32_t esz[256];           // switch link l: size of an echo crossing it (its sender's payload
+                                 // + 30 B: one hop on identity overlays, uniform on tunnelled ones)
+    uint32_t etx[256];           // ... and its transmission time (ns)
+    uint32_t abtx[256];          // access link of node u: transmission time of a big-signalling segment
+    uint32_t bpair[256];         // big-signalling generator g: source | destination << 8 | first link << 16
+    uint32_t fseq[512];          // start-event seq of flow slot f (data flows; slot F: generator 0)
+    int64_t  bs_period;          // generator send period (ns)
+    uint32_t n_bsig;             // generators (all in flow slot F)
+    uint32_t bs_nseg;            // segments per NN copy
+    uint32_t bs_size;            // segment size on the wire (542 B)
+    uint32_t pad_bs;
     // uint32_t route[N][N] follows (tunnelled overlays only): next link x -> y | hops(x, y) << 8
 };
 __host__ __device__ inline uint32_t ti_link(uint32_t ti) { return ti & 255u; }

@@ -508,6 +508,50 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
         return set_err(PRISMA_ERR_CONFIG, "sim_time_s must be in (0, 4095] (12-bit packet start second)");
     if (P->log_capacity < 1024 || P->log_capacity > (1u << 22) || (P->log_capacity & (P->log_capacity - 1)))
         return set_err(PRISMA_ERR_CONFIG, "log_capacity must be a power of two >= 1024");
+    if (P->signaling_type > PRISMA_SIGNALING_TARGET)
+        return set_err(PRISMA_ERR_CONFIG, "signaling_type must be PRISMA_SIGNALING_IDEAL, _NN or _TARGET");
+    // signalling (sim.cc:373-392): the echo payload of overlay node u by its overlay degree;
+    // a tunnelled overlay's echoes cross several links, which the engine sizes per link, so
+    // there the payload must be the same for every node
+    std::vector<uint32_t> epay(N, 0u);
+    for (int u = 0; u < N; ++u) {
+        const uint32_t od = (uint32_t)(OP.ovrow[u + 1] - OP.ovrow[u]);
+        epay[u] = P->signaling_type == PRISMA_SIGNALING_NN ? 8u + 8u * (od + 1u)
+                                                           : (P->signaling_type == PRISMA_SIGNALING_TARGET ? 24u : 0u);
+    }
+    if (OP.tunnels)
+        for (int i = 1; i < OP.NO; ++i)
+            if (epay[OP.ovnode[i]] != epay[OP.ovnode[0]])
+                return set_err(PRISMA_ERR_CONFIG, "signaling_type NN on a tunnelled overlay needs equal overlay "
+                                                  "degrees (echo sizes per node are modelled on identity overlays)");
+    // big signalling (sim.cc:634-647): one generator per flow between overlay neighbours, with
+    // --train and "NN"; each starts right after its flow (install order: fseq below)
+    const bool bsig = P->train && P->big_signaling && P->signaling_type == PRISMA_SIGNALING_NN;
+    std::vector<int32_t> gen_of(F, -1);
+    std::vector<uint32_t> bpair;
+    if (bsig) {
+        if (!(P->sync_step_s > 0.0f) || P->big_signaling_bytes == 0)
+            return set_err(PRISMA_ERR_CONFIG, "big signalling needs sync_step_s > 0 and big_signaling_bytes > 0");
+        for (int f = 0; f < F; ++f) {
+            const int u = T->flow_src[f], w = T->flow_dst[f];
+            for (int t = OP.ovrow[u]; t < OP.ovrow[u + 1]; ++t)
+                if ((int)ti_tgt(OP.tinfo[t]) == w) {
+                    gen_of[f] = (int32_t)bpair.size();
+                    bpair.push_back((uint32_t)u | ((uint32_t)w << 8) | (ti_link(OP.tinfo[t]) << 16));
+                    break;
+                }
+        }
+        if (bpair.size() > 256u) return set_err(PRISMA_ERR_CONFIG, "more than 256 big-signalling generators");
+    }
+    const int G = (int)bpair.size();
+    // ScheduleNextTx's period in the reference's arithmetic (big-signaling-application.cc:247-250):
+    // the uint32 size * 8 over the float syncStep is a float, 4096 over that a double
+    const float bs_rate = bsig ? (float)(P->big_signaling_bytes * 8u) / P->sync_step_s : 1.0f;
+    const int64_t bs_period = bsig ? sec_to_ns((double)(512u * 8u) / (double)bs_rate) : 0;
+    // (the generators share one event slot: a period must outlast an access-link transmission)
+    if (bsig && (bs_period < 1000 || bs_period >= ((int64_t)1 << 40)))
+        return set_err(PRISMA_ERR_CONFIG, "big-signalling period out of range [1 us, 2^40 ns)");
+    const uint32_t bs_size = 512u + 30u;
 
     memset(&L, 0, sizeof(L));
     const int Lk = E + N;
@@ -546,7 +590,8 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     // can be queued at once + the packets on the wire.
     double drain_s = (double)P->max_buffer_bytes * 8.0 / (double)P->link_bps + (double)L.sw_txd * 1e-9;
     const double tx_s = (double)L.sw_txd * 1e-9, ival = (double)P->ping_interval_s;
-    const uint32_t data_max = P->max_buffer_bytes / L.data_size;
+    // (a byte-limited FIFO holds the most packets when they are the smallest non-control ones)
+    const uint32_t data_max = P->max_buffer_bytes / (G && bs_size < L.data_size ? bs_size : L.data_size);
     std::vector<uint32_t> rcap(E);
     double span;
     if (!OP.tunnels) {
@@ -586,6 +631,13 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
         tot += rcap[l];
     }
     L.qcap_a = (uint32_t)(L.WCAP < 8 ? 8 : L.WCAP);
+    if (G) {                                         // all of a node's generators send at the same instants
+        std::vector<uint32_t> per(N, 0u);
+        uint32_t mx = 0;
+        for (uint32_t b : bpair) { const uint32_t c = ++per[b & 255u]; mx = c > mx ? c : mx; }
+        const uint32_t want = next_pow2(mx + 8u);
+        L.qcap_a = want > L.qcap_a ? want : L.qcap_a;
+    }
     tot += (uint32_t)N * L.qcap_a;
     L.ring_total = tot;
     // ping-back delay slots per responder: round k's slot is reused by round
@@ -616,13 +668,14 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     // register-resident engine: every limit of its fixed-size topology image,
     // lane-distributed registers and LDS image
     int fs = 1, ls = 1;
-    while (64 * fs < F) fs *= 2;
+    const int FG = F + (G ? 1 : 0);                  // flow slots: the generators share one (on_bsig)
+    while (64 * fs < FG) fs *= 2;
     while (64 * ls < (Lk > OP.T ? Lk : OP.T)) ls *= 2;
     const uint32_t reg_lds = 4u * (uint32_t)Lk * L.WCAP * (OP.tunnels ? 3u : 2u) + (OP.tunnels ? 0u : 4u * tot) +
                              4u * (uint32_t)OP.T * L.MA +
                              4u * (uint32_t)(OP.tunnels ? OP.n_resp : OP.T) * L.PBK + 1024u + 16u * (1u + L.W) +
                              (uint32_t)(N * N);
-    const bool reg_fits = N <= 255 && Lk <= 256 && E <= 256 && F <= 512 && OP.T <= 256 && fs <= 8 && ls <= 4 &&
+    const bool reg_fits = N <= 255 && Lk <= 256 && E <= 256 && FG <= 512 && OP.T <= 256 && fs <= 8 && ls <= 4 &&
                           tot <= 65535u && reg_lds + 256u <= 160u * 1024u;
     uint32_t engine = P->engine == PRISMA_ENGINE_AUTO ? (reg_fits ? PRISMA_ENGINE_REGISTER : PRISMA_ENGINE_MEMORY)
                                                       : P->engine;
@@ -631,6 +684,9 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
                                           "tunnels, 512 flows, 160 KiB LDS); use PRISMA_ENGINE_MEMORY");
     if (engine == PRISMA_ENGINE_MEMORY && OP.tunnels)
         return set_err(PRISMA_ERR_CONFIG, "the memory-resident engine runs identity overlays only");
+    if (engine == PRISMA_ENGINE_MEMORY && (P->signaling_type != PRISMA_SIGNALING_IDEAL || G))
+        return set_err(PRISMA_ERR_CONFIG, "the memory-resident engine runs signalling type \"ideal\" without big "
+                                          "signalling");
     uint32_t o = 0;
     auto take = [&](uint32_t bytes) { uint32_t r = o; o = align16(o + bytes); return r; };
     L.table_bytes = (uint32_t)(N * N);
@@ -662,9 +718,31 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     }
     if (OP.tunnels) memcpy(TI.tresp, OP.tresp.data(), 4u * OP.T);
     for (uint32_t c = 0; c < 8; ++c) {               // entry classes: relay, fresh, ping fwd, ping back, +echo bit
-        const bool data = (c & 2u) == 0u, echo = c == 7u;
-        TI.ctx[c] = (uint32_t)(data ? L.sw_txd : (echo ? L.sw_txe : L.sw_txp));
+        const bool data = (c & 2u) == 0u, echo = c == 7u, big = c == 6u;
+        TI.ctx[c] = (uint32_t)(data ? L.sw_txd : (echo ? L.sw_txe : (big ? sec_to_ns((double)bs_size * 8 / (double)P->link_bps)
+                                                                         : L.sw_txp)));
     }
+    for (int u = 0; u < N; ++u)                      // echoes leave node u on its own links
+        for (int l = T->row_ptr[u]; l < T->row_ptr[u + 1]; ++l) {
+            const uint32_t sz = (OP.tunnels ? epay[OP.ovnode[0]] : epay[u]) + 30u;
+            TI.esz[l] = sz;
+            TI.etx[l] = (uint32_t)sec_to_ns((double)sz * 8 / (double)P->link_bps);
+        }
+    for (int u = 0; u < N; ++u)
+        TI.abtx[u] = (uint32_t)sec_to_ns((double)bs_size * 8 / (double)((uint64_t)1000000 * P->link_bps * (uint64_t)pdeg[u]));
+    for (int g = 0; g < G; ++g) TI.bpair[g] = bpair[g];
+    {                                                // start events: ping timers, then apps in install order
+        uint32_t q = (uint32_t)OP.NO;
+        for (int f = 0; f < F; ++f) {
+            TI.fseq[f] = q++;
+            if (gen_of[f] == 0) TI.fseq[F] = q;      // generator 0 opens the group's slot
+            if (gen_of[f] >= 0) q++;
+        }
+    }
+    TI.bs_period = bs_period;
+    TI.n_bsig = (uint32_t)G;
+    TI.bs_nseg = bsig ? P->big_signaling_bytes / 512u : 0u;
+    TI.bs_size = bs_size;
     if (OP.tunnels) memcpy(topo.data() + sizeof(TopoImage), OP.route.data(), 4u * (size_t)N * N);
 
     // state image: LDS part (staged into LDS) then register part (staged into VGPRs)

@@ -18,7 +18,7 @@ from .topology import Topology
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprisma_amd.so")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 PRISMA_POLICY_TABLE = 1
 PRISMA_POLICY_DQN_BUFFER = 2
 PRISMA_ENGINE_AUTO, PRISMA_ENGINE_REGISTER, PRISMA_ENGINE_MEMORY = 0, 1, 2
@@ -49,8 +49,12 @@ class _Params(C.Structure):
         ("ma_size", C.c_uint32), ("ping_as_obs", C.c_uint32), ("auto_reset", C.c_uint32),
         ("loss_penalty", C.c_double), ("seed", C.c_uint64), ("replica_base", C.c_uint32),
         ("log_capacity", C.c_uint32), ("notify_dest", C.c_uint32), ("train", C.c_uint32),
-        ("engine", C.c_uint32),
+        ("engine", C.c_uint32), ("signaling_type", C.c_uint32), ("big_signaling", C.c_uint32),
+        ("sync_step_s", C.c_float), ("big_signaling_bytes", C.c_uint32),
     ]
+
+
+_PARAM_DEFAULTS = dict(engine=0, signaling_type=0, big_signaling=0, sync_step_s=1.0, big_signaling_bytes=35328)
 
 
 class _LogView(C.Structure):
@@ -165,7 +169,8 @@ def _topo_struct(topo: Topology):
 
 def _params_struct(params: dict) -> _Params:
     """prisma_params_t from an engine_params() dict (engine defaults to auto)."""
-    return _Params(**{k: params.get(k, 0) if k == "engine" else params[k] for k, _ in _Params._fields_})
+    return _Params(**{k: params.get(k, _PARAM_DEFAULTS[k]) if k in _PARAM_DEFAULTS else params[k]
+                      for k, _ in _Params._fields_})
 
 
 def plan(topo: Topology, params: dict) -> dict:

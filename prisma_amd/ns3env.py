@@ -102,11 +102,27 @@ class InfoTracker:
         return (self._stats(cnt, now, float(int(rec["start_s"])), self.data_size, uid, 0)
                 + f", Packet Lost={lost_ids}, Source={self.src.get(uid, v)}, Destination={int(rec['dst'])}, node={v}")
 
-    def render_ctrl(self, uid: int, cnt) -> str:
+    def render_ctrl(self, uid: int, cnt, size: int = 30) -> str:
         """SmallSignalingPacketManager::getInfo (small-signaling-packet-manager.cc:104-114): 20
-        tokens.  Token 3 (the echo's own ns-3 packet uid) carries the signalled uid."""
+        tokens.  Token 3 (the echo's own ns-3 packet uid) carries the signalled uid; size is the
+        echo's size on the wire (30 B + its payload by signalling type, sim.cc:373-392)."""
         now = int(cnt["now_ns"]) / 1e9
-        return self._stats(cnt, now, 0.0, 30, uid, 2) + f", PacketIdSignaled={uid}, Arrived at final dest=1"
+        return self._stats(cnt, now, 0.0, size, uid, 2) + f", PacketIdSignaled={uid}, Arrived at final dest=1"
+
+    def render_big(self, nn: int, seg: int, src_overlay: int, cnt) -> str:
+        """BigSignalingPacketManager::getInfo (big-signaling-packet-manager.cc:111-123): 21 tokens,
+        the NN-weight segment (542 B on the wire) of overlay node src_overlay.  Token 3 (the
+        segment's ns-3 packet uid) is not modelled: 0."""
+        now = int(cnt["now_ns"]) / 1e9
+        return (self._stats(cnt, now, 0.0, 542, 0, 1)
+                + f", NN Index={nn}, segment Index={seg}, NodeId Signaled={src_overlay}")
+
+    def render_control(self, row, cnt) -> str:
+        """Info string of a control notification from its engine obs row [1000, a, b, c]
+        (include/prisma.h, prisma_params_t.notify_dest)."""
+        if int(row[3]) & 0x10000:
+            return self.render_big(int(row[1]), int(row[2]), int(row[3]) & 0xFFFF, cnt)
+        return self.render_ctrl(int(row[1]), cnt, int(row[2]))
 
 
 class PrismaSession:
@@ -156,9 +172,9 @@ class PrismaSession:
         v = int(node.cpu()[0])
         row = obs.cpu().numpy()[0]
         if int(row[0]) == 1000:
-            # small-signalling (--train) notification: obs [1000]; GetGameOver reports the
-            # node's last data notification (packet-routing-gym.cc:143-148)
-            self._pending = (v, [1000], self._last_done[v], self.tracker.render_ctrl(int(row[1]), cnt), None)
+            # control notification (--train small signalling, --signaling big signalling): obs
+            # [1000]; GetGameOver reports the node's last data notification (packet-routing-gym.cc:143-148)
+            self._pending = (v, [1000], self._last_done[v], self.tracker.render_control(row, cnt), None)
         else:
             d = int(cnt["dec_count"]) - 1
             rec = self.engine.records(0, d, 1)[0]

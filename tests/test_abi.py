@@ -32,7 +32,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = engine.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.prisma_abi_version() == engine.ABI_VERSION == 6
+    assert lib.prisma_abi_version() == engine.ABI_VERSION == 7
     out = subprocess.run(["nm", "-D", "--defined-only", engine.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (prisma_\w+)", out))
     assert set(declared_functions()) <= exported
@@ -58,6 +58,8 @@ int main(void) {
          offsetof(prisma_params_t, log_capacity), offsetof(prisma_counters_t, cost_sum),
          offsetof(prisma_counters_t, hops_total));
   printf("%zu %zu %zu\n", offsetof(prisma_params_t, engine), sizeof(prisma_plan_t), offsetof(prisma_plan_t, engine));
+  printf("%zu %zu %zu %zu\n", offsetof(prisma_params_t, signaling_type), offsetof(prisma_params_t, big_signaling),
+         offsetof(prisma_params_t, sync_step_s), offsetof(prisma_params_t, big_signaling_bytes));
   return 0;
 }
 '''
@@ -80,6 +82,9 @@ def test_ctypes_layouts_match_header():
     assert offs[4] == COUNTERS_DTYPE.fields["hops_total"][1]
     eng = list(map(int, lines[2].split()))
     assert eng == [engine._Params.engine.offset, C.sizeof(engine._Plan), engine._Plan.engine.offset]
+    sig = list(map(int, lines[3].split()))
+    assert sig == [getattr(engine._Params, k).offset for k in
+                   ("signaling_type", "big_signaling", "sync_step_s", "big_signaling_bytes")]
 
 
 def test_engine_refuses_without_gpu():

@@ -70,20 +70,24 @@ def test_info_renderer_matches_oracle(oracle_mod):
     assert lost_seen > 0 and dest_seen > 0
 
 
-def test_control_info_renderer_matches_oracle(oracle_mod):
+@pytest.mark.parametrize("sig", [dict(), dict(signaling_type="target"),
+                                 dict(signaling_type="NN", big_signaling=1)])
+def test_control_info_renderer_matches_oracle(oracle_mod, sig):
     topo = Topology.example("abilene")
-    params = engine_params(topo, sim_time_s=2.0, ping_as_obs=1, notify_dest=1, train=1)
+    params = engine_params(topo, sim_time_s=2.0, ping_as_obs=1, notify_dest=1, train=1, **sig)
     o = oracle_mod.OracleSim(topo, params)
     tr = InfoTracker(topo.n_nodes, 542)
     pol = sp_policy(topo)
-    obs, n_ctrl = o.step(-1), 0
+    obs, n_ctrl, n_big = o.step(-1), 0, 0
     while obs is not None and n_ctrl < 300:
         v = o.pending_node()
         if int(obs[0]) == 1000:
-            assert tr.render_ctrl(int(obs[1]), o.counters()) == o.last_info()
+            assert tr.render_control(obs, o.counters()) == o.last_info()
             n_ctrl += 1
+            n_big += int(obs[3]) >> 16
         obs = o.step(pol(v, obs))
     assert n_ctrl == 300
+    assert (n_big > 0) == bool(sig.get("big_signaling"))
 
 
 def test_notify_dest_does_not_change_the_trajectory(oracle_mod):
@@ -100,12 +104,15 @@ def test_notify_dest_does_not_change_the_trajectory(oracle_mod):
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")
-@pytest.mark.parametrize("name,lf,train", [("abilene", 2.0, 0), ("abilene", 2.0, 1),
-                                           ("overlay_full_mesh_3n_abilene", 10.0, 1)])
-def test_session_stream_matches_oracle(oracle_mod, name, lf, train):
+@pytest.mark.parametrize("name,lf,train,sig", [("abilene", 2.0, 0, 0), ("abilene", 2.0, 1, 0),
+                                               ("overlay_full_mesh_3n_abilene", 10.0, 1, 0),
+                                               ("abilene", 1.0, 1, 1), ("overlay_full_mesh_3n_abilene", 10.0, 1, 1)])
+def test_session_stream_matches_oracle(oracle_mod, name, lf, train, sig):
     from prisma_amd.ns3env import PrismaSession
     topo = Topology.example(name, 0, lf)
     kw = dict(sim_time_s=2.0, ping_as_obs=1, train=train)
+    if sig:                                                        # "NN" echoes + big signalling
+        kw.update(signaling_type="NN", big_signaling=1, sync_step_s=0.25)
     pol = sp_policy(topo)
     _, ref = oracle_stream(oracle_mod, topo, engine_params(topo, notify_dest=1, **kw), pol, 1500)
     s = PrismaSession(topo=topo, base_port=7000, **kw)
