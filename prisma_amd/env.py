@@ -158,7 +158,7 @@ class VecRoutingEnv:
         empty = {k: torch.zeros((0,) + s, dtype=t, device=self.device) for k, s, t in
                  [("obs", (W,), torch.int32), ("action", (), torch.int32), ("reward", (), torch.float64),
                   ("next_obs", (W,), torch.int32), ("done", (), torch.bool), ("node", (), torch.int32),
-                  ("replica", (), torch.int32)]}
+                  ("replica", (), torch.int32), ("uid", (), torch.int64), ("hop", (), torch.bool)]}
         if total == 0:
             return empty
         rep = torch.repeat_interleave(torch.arange(self.R, device=self.device), n)
@@ -191,6 +191,11 @@ class VecRoutingEnv:
                                torch.ones(int(dr.sum()), dtype=torch.bool, device=self.device)]),
             "node": torch.cat([prev["node"], cur_f["node"][dr]]).to(torch.int32),
             "replica": torch.cat([rep_f[hp], rep_f[dr]]).to(torch.int32),
+            # the packet's uid and whether this is a hop transition (False: a loss transition):
+            # with "NN" / "target" signalling a hop transition waits for its echo (trainer.py)
+            "uid": torch.cat([cur_f["uid"][hp], cur_f["uid"][dr]]).to(torch.int64),
+            "hop": torch.cat([torch.ones(int(hp.sum()), dtype=torch.bool, device=self.device),
+                              torch.zeros(int(dr.sum()), dtype=torch.bool, device=self.device)]),
         }
         return out
 
