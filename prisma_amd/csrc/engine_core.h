@@ -901,7 +901,9 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
         const uint32_t l = tunnel_link(S, (uint32_t)(r0 + action));   // RouteOutput (:281-287)
         CNT_ADD(S, hops, 1u);
         CNT_ADD(S, hop_deg_sum, (uint64_t)deg);
-        const uint32_t src = ent_src(x, v);
+        // (memory-resident engine without the ctrl paths: the destination instead of the
+        // source, engine_layout.h)
+        const uint32_t src = (RS::kMem && !S.ctrl) ? dst : ent_src(x, v);
         const uint32_t fwd = (PRISMA_ABLATE & 1) ? (T_RELAY | (dst << 2) | (start << 10) | (src << 24)) : r_make(d, src);
         if (link_send(S, R, H, l, fwd)) {                         // lastHop = v, previous decision = d
             status = PRISMA_ST_ENQUEUED;
@@ -1096,6 +1098,8 @@ struct MlpPre1 {
     float b2;
     float4 wb[4];
     float b1v;
+    float w1v;                   // the one-hot row element, when the destination was known (has_w1)
+    bool has_w1;
 };
 
 __device__ __forceinline__ void mlp_preload(MlpPre& M, const float* __restrict__ RP, int lane, int D, int deg,
@@ -1116,16 +1120,19 @@ __device__ __forceinline__ void mlp_preload(MlpPre& M, const float* __restrict__
     M.b4 = lane < deg ? RP[2 * mlp_rp_layer_floats(64) + 64 * D + lane] : 0.0f;
 }
 
-// every weight a decision at node v reads except its one-hot row (which needs the
-// destination): issued by the memory-resident engine's arrival handler together with
+// layers 1-2 of a decision at node v (the one-hot row too when the destination dst is
+// known, has_w1): issued by the memory-resident engine's arrival handler together with
 // its second round trip (previous decision record, observation), so the decision finds
 // them in registers
-__device__ __forceinline__ void mlp_preload_node(MlpPre1& M, const Sim& S, uint32_t v) {
+__device__ __forceinline__ void mlp_preload_node(MlpPre1& M, const Sim& S, uint32_t v, uint32_t dst, bool has_w1) {
     const int lane = S.lane;
     const int D = S.lv.max_deg();
     const float* __restrict__ RP1 = S.mlp_rp + (size_t)v * mlp_rp_node_floats(D);
     const float* __restrict__ RP = RP1 + mlp_rp_l1_floats(D);
     const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
+    M.has_w1 = has_w1;
+    M.w1v = 0.0f;
+    if (has_w1 && lane < 32) M.w1v = S.mlp[((int)v * S.lv.N() + (int)dst) * 32 + (lane & 31)];
 #pragma unroll
     for (int c = 0; c < 16; ++c) M.w2[c] = ((const float4*)RP)[c * 64 + lane];
     M.b2 = RP[64 * 64 + lane];
@@ -1169,15 +1176,19 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
 #endif
     const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
     const uint32_t dst = rdl(obs_reg, 0);
-    MlpPre M;
-    if constexpr (B == kMlpAll) mlp_preload(M, RP, lane, D, deg, !PRE);   // PRE: layer 2 came with the arrival
     // layer-1 weights first (independent of the normalisation): one W1 row element and
     // b1 for the one-hot branch (lanes 0-31), the Wb chunks and bb for the buffers branch
-    // (lanes 32-63; deg <= D, so at most ceil(D/4) chunks)
+    // (lanes 32-63; deg <= D, so at most ceil(D/4) chunks).  The row element is issued
+    // before the layer 3-4 loads: the in-order load counter makes layer 1 wait for
+    // everything issued before it.
     const int j32 = lane & 31;
     const int nck = (deg + 3) >> 2;
     const float4* __restrict__ Wb4 = (const float4*)RP1;
-    const float w1v = (lane < 32) ? W1[((int)v * N + (int)dst) * 32 + j32] : 0.0f;
+    float w1v;
+    if (PRE && P1.has_w1) w1v = P1.w1v;
+    else w1v = (lane < 32) ? W1[((int)v * N + (int)dst) * 32 + j32] : 0.0f;
+    MlpPre M;
+    if constexpr (B == kMlpAll) mlp_preload(M, RP, lane, D, deg, !PRE);   // PRE: layer 2 came with the arrival
     float b1v;
     float4 wb[4];
     if constexpr (PRE) {
@@ -1371,7 +1382,16 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap() - 1)) * L.rec_bytes();
         const uint4 ph = *(const uint4*)pr;
         const uint2 pw = *(const uint2*)(pr + 24);
-        if constexpr (PRE) mlp_preload_node(Mpre, S, v);          // the decision's weights ride along
+        if constexpr (PRE) {                                        // the decision's weights ride along
+            if (S.ctrl) {
+                mlp_preload_node(Mpre, S, v, 0u, false);
+            } else {
+                // the entry names the destination (engine_layout.h): no weights for a
+                // packet that has arrived, the one-hot row element with the others
+                const uint32_t dst_e = (type == T_FRESH) ? f_dst(x) : r_dst(x);
+                if (dst_e != v) mlp_preload_node(Mpre, S, v, dst_e, true);
+            }
+        }
         // memory-resident engine: the observation's gather goes out with the record
         // load, before the arrival link's update (it reads node v's out-links, which
         // nothing touches before the decision)

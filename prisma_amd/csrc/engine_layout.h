@@ -16,7 +16,10 @@ constexpr uint32_t K_PING = 0u, K_FLOW = 1u, K_COMPLETE = 2u, K_ARRIVE = 3u;
 //            index mod 2^22, bits 24-31 = the packet's source node (its uid,
 //            destination, start second, TTL, decision time and -- through the
 //            deciding node and action -- its tunnel are read back from the
-//            decision record in the HBM log)
+//            decision record in the HBM log).  The memory-resident engine's
+//            kernels without the --train / notify_dest paths (which never read
+//            the source back) carry the destination there instead, so an
+//            arrival knows it before the record load returns (r_dst)
 //   T_FRESH  data packet of a flow app on its access link: bits 2-9 its
 //            destination, bit 10 parity of the start second, bits 11-31 uid
 //            mod 2^21 (its source is the switch it arrives at)
@@ -47,6 +50,7 @@ __host__ __device__ inline uint32_t r_make(uint32_t dec, uint32_t src) {
 }
 __host__ __device__ inline uint32_t r_dec(uint32_t x) { return (x >> 2) & ((1u << 22) - 1u); }
 __host__ __device__ inline uint32_t r_src(uint32_t x) { return x >> 24; }
+__host__ __device__ inline uint32_t r_dst(uint32_t x) { return x >> 24; }   // (memory-resident, no ctrl)
 __host__ __device__ inline uint32_t f_make(uint32_t dst, uint32_t start_parity, uint32_t uid) {
     return T_FRESH | (dst << 2) | (start_parity << 10) | (uid << 11);
 }
