@@ -289,6 +289,7 @@ struct Sim {
     unsigned char* logrep;
     uint32_t gid;
     int lane;
+    uint32_t m1, m2, m4, m8;                // per-lane word masks -(lane & 1), -(lane>>1 & 1), -(lane>>2 & 1), -(lane < 8)
     bool tun;                               // tunnelled overlay: a compile-time constant in the
                                             // step kernels (template TUN), folded after inlining
     bool mem;                               // memory-resident engine (compile-time constant, folded)
@@ -331,6 +332,13 @@ __device__ inline void sim_bind(Sim& S, const LV& L, unsigned char* lds, const u
     S.logrep = logrep;
     S.gid = gid;
     S.lane = lane;
+    // opaque to the optimiser, so write_record's selects stay bitfield inserts on VGPR masks
+    // instead of loop-invariant lane-compare SGPR pairs (which the headline kernel spilled)
+    S.m1 = 0u - ((uint32_t)lane & 1u);
+    S.m2 = 0u - (((uint32_t)lane >> 1) & 1u);
+    S.m4 = 0u - (((uint32_t)lane >> 2) & 1u);
+    S.m8 = lane < 8 ? ~0u : 0u;
+    asm volatile("" : "+v"(S.m1), "+v"(S.m2), "+v"(S.m4), "+v"(S.m8));
     S.tun = L.tunnels() != 0u;
     S.mem = false;
     S.ctrl = true;
@@ -803,15 +811,18 @@ __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_
     uint32_t w7 = (uint32_t)(uint8_t)(int8_t)action | (status << 8) | (ttl << 16) | ((H.episode & 0xffu) << 24);
     // lane l < 8 picks header word l with three lane-bit selects, no per-lane compares
     // (A/B +3.5 % at the headline against a switch on the lane id)
-    const uint32_t a01 = (lane & 1) ? hi32(H.now) : lo32(H.now);
-    const uint32_t a23 = (lane & 1) ? (uint32_t)prev : uid;
-    const uint32_t a45 = (lane & 1) ? (uint32_t)(rb >> 32) : (uint32_t)rb;
-    const uint32_t a67 = (lane & 1) ? w7 : (node | (dst << 8) | (start << 16));
-    const uint32_t a03 = (lane & 2) ? a23 : a01;
-    const uint32_t a47 = (lane & 2) ? a67 : a45;
-    const uint32_t hw = (lane & 4) ? a47 : a03;
+    // (bitfield inserts on the per-lane masks, v_bfi_b32: A/B +1.4 % at the headline against
+    // lane-bit selects, whose loop-invariant SGPR-pair conditions were spilled and reloaded)
+    auto bfi = [](uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); };
+    const uint32_t a01 = bfi(S.m1, hi32(H.now), lo32(H.now));
+    const uint32_t a23 = bfi(S.m1, (uint32_t)prev, uid);
+    const uint32_t a45 = bfi(S.m1, (uint32_t)(rb >> 32), (uint32_t)rb);
+    const uint32_t a67 = bfi(S.m1, w7, node | (dst << 8) | (start << 16));
+    const uint32_t a03 = bfi(S.m2, a23, a01);
+    const uint32_t a47 = bfi(S.m2, a67, a45);
+    const uint32_t hw = bfi(S.m4, a47, a03);
     uint32_t ob = bperm(obs_reg, (uint32_t)(lane - 8) & 63u);
-    uint32_t word = lane < 8 ? hw : ob;
+    uint32_t word = bfi(S.m8, hw, ob);
     uint32_t* p = (uint32_t*)(S.logrep + (size_t)(d & (S.lv.log_cap() - 1)) * S.lv.rec_bytes());
     if (lane < 8 + S.lv.W()) p[lane] = word;
 }
