@@ -294,6 +294,7 @@ struct Sim {
                                             // step kernels (template TUN), folded after inlining
     bool mem;                               // memory-resident engine (compile-time constant, folded)
     bool ctrl;                              // --train echo / notify_dest paths compiled in (constant)
+    bool mlp_inst;                          // an in-kernel MLP instance (event_loop's MLP, constant)
     // memory-resident engine: variable-size topology arrays (scalar loads)
     const CAS int32_t* m_rowptr;
     const CAS int32_t* m_ldst;
@@ -342,6 +343,7 @@ __device__ inline void sim_bind(Sim& S, const LV& L, unsigned char* lds, const u
     S.tun = L.tunnels() != 0u;
     S.mem = false;
     S.ctrl = true;
+    S.mlp_inst = false;
     S.lrec = nullptr;
 }
 
@@ -991,10 +993,11 @@ __device__ __forceinline__ void on_ping_round(const Sim& S, RS& R, Hot& H) {   /
 template <class RS>
 __device__ __forceinline__ void flow_next(const Sim& S, RS& R, Hot& H, uint32_t f, uint32_t draw) {
     uint32_t c[4] = { f, draw, H.episode, 1u };                   // poisson-application.cc:265-295
-    // the key is opaque here, so its ten round keys are derived per call (two s_add a round)
-    // instead of hoisted out of the event loop into 18 SGPRs (A/B +0.6 % at the headline)
+    // table-policy instances: the key is opaque here, so its ten round keys are derived per
+    // call (two s_add a round) instead of hoisted out of the event loop into 18 SGPRs (A/B
+    // +0.6 % at the headline); the MLP instances keep them hoisted (opaque: config 4 -2.5 %)
     uint32_t k0 = S.lv.seed_lo(), k1 = S.gid;
-    asm volatile("" : "+s"(k0), "+s"(k1));
+    if (!S.mlp_inst) asm volatile("" : "+s"(k0), "+s"(k1));
     philox4x32_10(c, k0, k1);
     uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
     double U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
@@ -1806,6 +1809,7 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
     const int lane = S.lane;
     const LV& L = S.lv;
     const bool mlp_mode = MLP;
+    S.mlp_inst = MLP;
     const bool table_mode = (P.mode == 2) || mlp_mode;            // fused in-kernel policy
     S.mlp = P.mlp;
     S.mlp_rp = P.mlp_rp;
