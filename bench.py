@@ -60,6 +60,15 @@ def parse():
     p.add_argument("--cpu-hops-1core", type=int, default=4000000, help="oracle hops of the single-thread pass")
     p.add_argument("--same-device", action="store_true",
                    help="N ranks share cuda:0 over gloo (rehearsal of the N-rank path on one GPU)")
+    p.add_argument("--rank-deadline", type=float, default=None,
+                   help="seconds the N-rank launcher waits for every rank to finish before it terminates them "
+                        "all and names the ranks that had not reported (default: init allowance + a per-step "
+                        "bound x (warmup + steps) + the CPU-baseline allowance)")
+    p.add_argument("--rendezvous-only", action="store_true",
+                   help="ranks only initialise torch.distributed and all-gather their replica counts (no GPU "
+                        "work unless the backend is nccl): a check of the N-rank plumbing")
+    p.add_argument("--backend", default=None, choices=["nccl", "gloo"],
+                   help="process-group backend (default: nccl = RCCL; gloo with --same-device)")
     a = p.parse_args()
     big = a.topology == "er256"
     if a.replicas is None:
@@ -178,19 +187,61 @@ def issue_roofline(topology: str, replicas: int, hops: int, build: str):
     return {k: e[k] for k in keys if k in e}
 
 
-def launch_ranks(n: int) -> int:
+INIT_ALLOWANCE_S = 240.0      # first `import torch` on a fresh box (1-2 min) + RCCL init
+STEP_BOUND_S = 5.0            # per launch: the slowest BASELINE workload takes ~0.15 s
+CPU_BASELINE_ALLOWANCE_S = 120.0
+RANK_STAGES = ("started", "init", "timed", "done")
+
+
+def rank_deadline(args) -> float:
+    if args.rank_deadline is not None:
+        return float(args.rank_deadline)
+    return INIT_ALLOWANCE_S + STEP_BOUND_S * (args.warmup + args.steps) + CPU_BASELINE_ALLOWANCE_S
+
+
+def report_stage(stage: str) -> None:
+    """Tell the launcher (launch_ranks) that this rank reached `stage` (a marker file)."""
+    d = os.environ.get("PRISMA_BENCH_REPORT_DIR")
+    if d:
+        with open(os.path.join(d, f"rank{os.environ.get('RANK', '0')}.{stage}"), "w") as fh:
+            fh.write(f"{time.time()}\n")
+
+
+def launch_ranks(n: int, deadline_s: float) -> int:
     """Start n child ranks of this script (one per GPU) and wait for them.  The parent touches no
     GPU (no torch import at all) and does not exec: it runs the ranks as subprocesses with the
-    torch.distributed env contract and returns the worst exit status; a failing rank stops the rest."""
+    torch.distributed env contract and returns the worst exit status; a failing rank stops the rest.
+    Each rank reports its stages (started, init, timed, done) as marker files; if the ranks are not
+    all finished `deadline_s` after the start, every rank is terminated (killed after a 10-s grace),
+    the ranks that had not reached "done" are named with their last stage, and the exit status is 124."""
+    import tempfile
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
+    rep = tempfile.mkdtemp(prefix="prisma_bench_ranks_")
     procs = []
+    t_start = time.monotonic()
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PRISMA_BENCH_REPORT_DIR=rep)
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+
+    def last_stage(r):
+        got = [st for st in RANK_STAGES if os.path.exists(os.path.join(rep, f"rank{r}.{st}"))]
+        return got[-1] if got else "not started"
+
+    def stop_all(live):
+        for q in live:
+            q.terminate()
+        t_kill = time.monotonic() + 10.0
+        for q in live:
+            try:
+                q.wait(timeout=max(0.1, t_kill - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                q.kill()
+                q.wait()
+
     rc = 0
     live = list(procs)
     while live:
@@ -201,23 +252,68 @@ def launch_ranks(n: int) -> int:
             live.remove(p)
             if c != 0:
                 rc = rc or c
-                for q in live:
-                    q.terminate()
+                stop_all(live)
+                live = []
+        if live and time.monotonic() - t_start > deadline_s:
+            stuck = [f"rank {r} (last stage: {last_stage(r)})" for r, p in enumerate(procs) if p in live]
+            print(f"bench.py: rank deadline of {deadline_s:.0f} s expired; not finished: {', '.join(stuck)}; "
+                  f"terminating all {n} ranks", file=sys.stderr, flush=True)
+            stop_all(live)
+            live = []
+            rc = 124
         time.sleep(0.2)
+    for f in os.listdir(rep):
+        os.unlink(os.path.join(rep, f))
+    os.rmdir(rep)
     return rc
+
+
+def rendezvous_only(args, world: int, rank: int) -> None:
+    """--rendezvous-only: initialise the process group, all-gather each rank's replica count and
+    print one JSON line on rank 0 (a check of the N-rank plumbing: spawn, rendezvous, collective)."""
+    import torch
+    import torch.distributed as dist
+    from prisma_amd.dist import shard
+    backend = args.backend or ("gloo" if args.same_device else "nccl")
+    if backend == "nccl":
+        dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
+        torch.cuda.set_device(dev)
+        dist.init_process_group("nccl", device_id=dev)
+    else:
+        dev = torch.device("cpu")
+        dist.init_process_group("gloo")
+    report_stage("init")
+    _, R = shard(args.replicas * world, rank, world)
+    t = torch.zeros(world, dtype=torch.int64, device=dev)
+    t[rank] = R
+    dist.all_reduce(t)
+    report_stage("timed")
+    if rank == 0:
+        print(json.dumps({"rendezvous": "ok", "backend": backend, "world_size": dist.get_world_size(),
+                          "replicas_gathered": int(t.sum().item()), "per_rank_replicas": t.cpu().tolist()}),
+              flush=True)
+    dist.destroy_process_group()
+    report_stage("done")
 
 
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(launch_ranks(args.gpus))
+        sys.exit(launch_ranks(args.gpus, rank_deadline(args)))
+    report_stage("started")
+    stall = os.environ.get("PRISMA_BENCH_STALL_RANK")       # test hook: this rank hangs before init
+    if stall is not None and stall == os.environ.get("RANK"):
+        time.sleep(3600)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if args.rendezvous_only:
+        rendezvous_only(args, world, rank)
+        return
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     local = 0 if args.same_device else int(os.environ.get("LOCAL_RANK", "0"))
-    backend = "gloo" if args.same_device else "nccl"
+    backend = args.backend or ("gloo" if args.same_device else "nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     if world > 1:
@@ -226,6 +322,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+    report_stage("init")
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
     from prisma_amd.config import engine_params
@@ -278,6 +375,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    report_stage("timed")
     elapsed = t1 - t0
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
@@ -342,6 +440,8 @@ def main():
                 "issue": issue_roofline(args.topology, args.replicas, args.hops, bid),
             },
             "errors": errors,
+            "dist": {"world_size": dist.get_world_size() if world > 1 else 1, "backend": backend if world > 1 else None,
+                     "replicas_gathered": int(stats["stats"].shape[0])},
             "episodes_completed": stats["episodes_completed"],
             "replicas_total": int(stats["stats"].shape[0]),
             "per_rank_hops_s": [h / elapsed for h in per_rank],
@@ -353,6 +453,7 @@ def main():
     eng.close()
     if world > 1:
         dist.destroy_process_group()
+    report_stage("done")
 
 
 if __name__ == "__main__":

@@ -62,6 +62,11 @@ def lib():
         L.or_run_mlp.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
         L.or_mlp_action.restype = C.c_int32
         L.or_mlp_action.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p]
+        L.or_mlp_q.restype = C.c_int32
+        L.or_mlp_q.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+        L.or_mlp_q_batch.restype = None
+        L.or_mlp_q_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int32,
+                                     C.c_void_p, C.c_int32, C.c_void_p]
         L.or_det_expm1.restype = C.c_double
         L.or_det_expm1.argtypes = [C.c_double]
         L.or_det_expm1f.restype = C.c_float
@@ -223,6 +228,26 @@ class OracleSim:
         w = np.ascontiguousarray(weights, dtype=np.float32)
         o = np.ascontiguousarray(obs, dtype=np.uint32)
         return int(lib().or_mlp_action(self.h, w.ctypes.data, int(node), o.ctypes.data))
+
+    def mlp_q(self, weights: np.ndarray, node: int, obs) -> np.ndarray:
+        """The restatement's fixed-order fp32 Q values (length = the node's degree)."""
+        w = np.ascontiguousarray(weights, dtype=np.float32)
+        o = np.ascontiguousarray(obs, dtype=np.uint32)
+        q = np.zeros(max(self.topo.max_deg, 1), dtype=np.float32)
+        lib().or_mlp_q(self.h, w.ctypes.data, int(node), o.ctypes.data, q.ctypes.data)
+        return q[:int(self.topo.degrees[node])]
+
+    def mlp_q_batch(self, weights: np.ndarray, nodes, obs):
+        """(Q [n, max_deg] with +inf past each node's degree, actions [n]) of the restatement."""
+        w = np.ascontiguousarray(weights, dtype=np.float32)
+        nd = np.ascontiguousarray(nodes, dtype=np.int32)
+        o = np.ascontiguousarray(obs, dtype=np.uint32)
+        D = max(self.topo.max_deg, 1)
+        q = np.full((nd.size, D), np.inf, dtype=np.float32)
+        a = np.zeros(nd.size, dtype=np.int32)
+        lib().or_mlp_q_batch(self.h, w.ctypes.data, nd.size, nd.ctypes.data, o.ctypes.data, o.shape[1],
+                             q.ctypes.data, D, a.ctypes.data)
+        return q, a
 
     def pending_node(self) -> int:
         return int(lib().or_pending_node(self.h))

@@ -1031,7 +1031,7 @@ static float elu_f(float x) { return x > 0.0f ? x : or_det_expm1f(x); }
 
 /* Packed weights (float): W1[N][N][32] b1[N][32] Wb[N][D][32] bb[N][32] W2[N][64][64] b2[N][64]
  * W3[N][64][64] b3[N][64] W4[N][64][D] b4[N][D], D = max_deg (prisma_amd.policies.StackedQNet.pack). */
-static int mlp_action(const or_sim_t* s, const float* w, int v, const uint32_t* obs) {
+static int mlp_action(const or_sim_t* s, const float* w, int v, const uint32_t* obs, float* q_out) {
     const int N = s->N, D = s->c.max_deg;
     const float* W1 = w;
     const float* b1 = W1 + (size_t)N * N * 32;
@@ -1075,6 +1075,7 @@ static int mlp_action(const or_sim_t* s, const float* w, int v, const uint32_t* 
         float acc = 0.0f;
         for (int i = 0; i < 64; ++i) acc = fmaf(h[i], W4[((size_t)v * 64 + i) * D + a], acc);
         float q = elu_f(acc + b4[v * D + a]);
+        if (q_out) q_out[a] = q;
         if (a == 0 || q < bq) { bq = q; best = a; }          /* tf.argmin: first minimum */
     }
     return best;
@@ -1086,7 +1087,7 @@ int64_t or_run_mlp(or_sim_t* s, const float* weights, int64_t max_hops) {
         if (s->pend) {
             rec_head_t* r = rec_at(s, s->pend_rec);
             const uint32_t* o = (const uint32_t*)((unsigned char*)r + sizeof(rec_head_t));
-            finish_data_decision(s, mlp_action(s, weights, r->node, o));
+            finish_data_decision(s, mlp_action(s, weights, r->node, o, NULL));
             continue;
         }
         if (!run_until_decision(s)) break;
@@ -1095,7 +1096,20 @@ int64_t or_run_mlp(or_sim_t* s, const float* weights, int64_t max_hops) {
 }
 
 int32_t or_mlp_action(or_sim_t* s, const float* weights, int32_t v, const uint32_t* obs) {
-    return mlp_action(s, weights, v, obs);
+    return mlp_action(s, weights, v, obs, NULL);
+}
+
+/* The fixed-order fp32 Q values of the same decision (q_out[0..deg-1]); returns the action. */
+int32_t or_mlp_q(or_sim_t* s, const float* weights, int32_t v, const uint32_t* obs, float* q_out) {
+    return mlp_action(s, weights, v, obs, q_out);
+}
+
+/* n decisions at once: nodes[n], obs[n][obs_stride], q_out[n][q_stride] (unused slots
+ * untouched), actions[n]. */
+void or_mlp_q_batch(or_sim_t* s, const float* weights, int64_t n, const int32_t* nodes, const uint32_t* obs,
+                    int32_t obs_stride, float* q_out, int32_t q_stride, int32_t* actions) {
+    for (int64_t i = 0; i < n; ++i)
+        actions[i] = mlp_action(s, weights, nodes[i], obs + i * obs_stride, q_out + i * q_stride);
 }
 
 int64_t or_record_count(const or_sim_t* s) { return s->rec_n; }

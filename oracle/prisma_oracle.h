@@ -81,6 +81,10 @@ int or_step(or_sim_t* s, int32_t action, int32_t* obs_out);
  * packed fp32 weights (layout: prisma_amd.policies.StackedQNet.pack). */
 int64_t or_run_mlp(or_sim_t* s, const float* weights, int64_t max_hops);
 int32_t or_mlp_action(or_sim_t* s, const float* weights, int32_t v, const uint32_t* obs);
+/* the same decision's fixed-order fp32 Q values into q_out[0..deg-1]; returns the action */
+int32_t or_mlp_q(or_sim_t* s, const float* weights, int32_t v, const uint32_t* obs, float* q_out);
+void or_mlp_q_batch(or_sim_t* s, const float* weights, int64_t n, const int32_t* nodes, const uint32_t* obs,
+                    int32_t obs_stride, float* q_out, int32_t q_stride, int32_t* actions);
 double or_det_expm1(double x);
 float or_det_expm1f(float x);
 

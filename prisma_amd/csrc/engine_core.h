@@ -72,7 +72,9 @@ struct KParams {
     int32_t R;
     int32_t max_hops;
     uint32_t episode;            // reset kernel only
-    int32_t mode;                // 0 reset, 1 external step, 2 table run
+    int32_t mode;                // 0 reset, 1 external step, 2 table run, 3 auto-reset, 4 MLP run
+    unsigned char* spare;        // [R][state_bytes] next-episode images (register engine with
+                                 // auto_reset), or null
 };
 
 // ---------------------------------------------------------------------------
@@ -1800,12 +1802,55 @@ __device__ __forceinline__ void publish_counters(const Sim& S, const KParams& P,
 }
 
 // ---------------------------------------------------------------------------
+// Episode boundaries inside a fused launch (prisma_run with auto_reset, register-resident
+// engine): main.py:111-114 runs the episodes back to back, so a replica whose episode ends
+// (Simulator::Stop at simTime, sim.cc:703) with hop budget left starts its next episode in the
+// same launch and spends the rest of its budget there.  The next episode's fresh image (LDS
+// part + register part) is built ahead of time by the reset kernel into P.spare, so the restart
+// is a copy: the LDS image and the registers are reloaded from it, and the log position and
+// the running totals carried over.  Built in place instead (init_replica's Philox draws inside
+// the loop, or an outer loop around the event loop, or an out-of-line call) the restart cost
+// the event loop its register allocation (scripts/asm_headline.sh: 24-60 VGPR spills).
+// Without a valid spare (two episode ends in one launch) the launch stops at the end as
+// before and the reset kernel after it starts the next episode.
+// ---------------------------------------------------------------------------
+template <int FS, int LS>
+__device__ __forceinline__ bool spare_restart(const KParams& P, Sim& S, Regs<FS, LS>& R, Hot& H, int r,
+                                              uint32_t& max_hops) {
+    if (!P.spare || H.error || H.hops_launch >= max_hops) return false;
+    CLayout& LC = *(CLayout*)P.lay;
+    const unsigned char* sp = P.spare + (size_t)r * LC.state_bytes;
+    if (rfl(((const Hdr*)(sp + kOffHdr))->episode) != H.episode + 1u) return false;
+    const int lane = S.lane;
+    const uint32_t dec = H.dec;
+    const uint64_t ht = (uint64_t)u_ld64((const int64_t*)&S.h->hops_total) + H.hops_launch;
+    const uint64_t et = (uint64_t)u_ld64((const int64_t*)&S.h->events_total) + H.ev_launch;
+    __syncthreads();
+    const uint4* s4 = (const uint4*)sp;
+    uint4* d4 = (uint4*)S.base;
+    for (uint32_t i = (uint32_t)lane; i < LC.lds_state_bytes / 16u; i += kWave) d4[i] = s4[i];
+    regs_io(R, (uint32_t*)(const_cast<unsigned char*>(sp) + LC.s_regs), lane, false);
+    __syncthreads();
+    if (lane == 0) {
+        S.h->dec_count = dec; S.h->hops_total = ht; S.h->events_total = et;
+        S.c->dec_count = dec; S.c->hops_total = ht; S.c->events_total = et;
+    }
+    __syncthreads();
+    max_hops -= H.hops_launch;
+    hot_load(S, H);                                      // the new episode: clock 0, nothing pending
+    flow_min_refresh(S, R, H);
+    return true;
+}
+template <class RS>
+__device__ __forceinline__ bool spare_restart(const KParams&, Sim&, RS&, Hot&, int, uint32_t&) { return false; }
+
+// ---------------------------------------------------------------------------
 // the event loop of one launch (both engines): finish the pending decision,
 // then one discrete event per iteration until max_hops hops, a decision that
 // needs an external action, or the end of the episode; publish the outputs.
 // ---------------------------------------------------------------------------
 template <bool MLP, int MB, class RS>
-__device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int r) {
+__device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, int r, uint32_t max_hops) {
     const int lane = S.lane;
     const LV& L = S.lv;
     const bool mlp_mode = MLP;
@@ -1815,7 +1860,6 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
     S.mlp_rp = P.mlp_rp;
     S.table_g = P.table;
     S.tab_lds = S.tab_lds && ((CLayout*)P.lay)->table_in_lds != 0u;
-    const uint32_t max_hops = (uint32_t)P.max_hops;
     const uint32_t NN = (uint32_t)L.N();
     Hot H;
     hot_load(S, H);
@@ -1864,6 +1908,8 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
         if (bt >= L.t_end()) {                           // Simulator::Stop(simTime) (sim.cc:703)
             lazy_resolve(S, R, H, true);                 // here, not after the loop: there it costs registers
             H.over = 1;
+            // fused run with auto_reset: the next episode starts here, from its prebuilt image
+            if (table_mode && spare_restart(P, S, R, H, r, max_hops)) continue;
             H.stop = 1;
             break;
         }
@@ -1939,4 +1985,5 @@ __device__ __forceinline__ void event_loop(const KParams& P, Sim& S, RS& R, int 
     if (P.node_out && lane == 0) P.node_out[r] = pending ? (int32_t)S.h->pend_node : -1;
     if (P.obs_out && lane < L.W()) P.obs_out[(size_t)r * L.W() + lane] = pending ? (int32_t)S.obs[lane] : 0;
     publish_counters(S, P, r, lane);
+    return H.hops_launch;
 }

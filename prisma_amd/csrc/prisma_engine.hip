@@ -43,38 +43,67 @@ const void* prisma_mem_kernel(int which, bool ctrl);
 
 
 // mode 0: (re)build every replica at episode P.episode.
-// mode 3 (auto-reset, launched after each step when auto_reset is set): a
-// replica whose episode ended (and did not fail) starts episode + 1, keeping
-// its decision-log position and running totals.  The event loop itself never
-// resets, so a launch never crosses an episode boundary.
+// mode 3 (auto-reset, launched after each prisma_step / prisma_run when auto_reset is set):
+// a replica whose episode ended (and did not fail) starts episode + 1, keeping its
+// decision-log position and running totals.  A fused run normally does this inside the step
+// kernel from the spare image (engine_core.h spare_restart); this catches the rest.
+// With P.spare (auto_reset), both modes also (re)build each replica's spare -- the fresh
+// image of the episode after its current one -- unless it is already there.
+template <int FS, int LS>
+__device__ __forceinline__ void image_store(const unsigned char* lds, CLayout& LC, unsigned char* img, int lane,
+                                            Regs<FS, LS>& R) {
+    uint4* s4 = (uint4*)img;
+    const uint4* d4 = (const uint4*)lds;
+    for (uint32_t i = (uint32_t)lane; i < LC.lds_state_bytes / 16u; i += kWave) s4[i] = d4[i];
+    regs_io(R, (uint32_t*)(img + LC.s_regs), lane, true);
+}
+
 template <int FS, int LS>
 __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
     CLayout& LC = *(CLayout*)P.lay;
-    const unsigned char* img = P.state + (size_t)r * LC.state_bytes;
+    unsigned char* img = P.state + (size_t)r * LC.state_bytes;
     const Hdr* gh = (const Hdr*)(img + kOffHdr);
-    uint32_t episode = P.episode;
-    Hot H;
-    memset(&H, 0, sizeof(H));
-    const bool keep = (P.mode == 3);
-    if (keep) {
-        if (!rfl(gh->over) || rfl(gh->error)) return;           // replica still running (or failed)
-        episode = rfl(gh->episode) + 1u;
-        H.dec = rfl(gh->dec_count);
-        if (lane < (int)(sizeof(Hdr) / 4)) ((uint32_t*)(lds + kOffHdr))[lane] = ((const uint32_t*)gh)[lane];
-        __syncthreads();
-    }
     LV lv;
     lv.load(P.lay, lane);
     Sim S;
     sim_bind(S, lv, lds, P.topo, P.log + (size_t)r * LC.log_cap * LC.rec_bytes, LC.replica_base + (uint32_t)r, lane);
-    Regs<FS, LS> R;
-    init_replica(S, R, H, episode, keep);
-    hot_store(S, R, H);
-    __syncthreads();
-    publish_counters(S, P, r, lane);
-    stage_out(lds, P, r, lane, R);
+    Hot H;
+    memset(&H, 0, sizeof(H));
+    const bool keep = (P.mode == 3);
+    uint32_t episode = P.episode;                        // the state's episode after this kernel
+    bool build = true;
+    if (keep) {
+        build = rfl(gh->over) && !rfl(gh->error);       // else: still running (or failed)
+        episode = rfl(gh->episode) + (build ? 1u : 0u);
+        if (build) {
+            H.dec = rfl(gh->dec_count);
+            if (lane < (int)(sizeof(Hdr) / 4)) ((uint32_t*)(lds + kOffHdr))[lane] = ((const uint32_t*)gh)[lane];
+            __syncthreads();
+        }
+    }
+    if (build) {
+        Regs<FS, LS> R;
+        init_replica(S, R, H, episode, keep);
+        hot_store(S, R, H);
+        __syncthreads();
+        publish_counters(S, P, r, lane);
+        image_store(lds, LC, img, lane, R);
+    }
+    if (P.spare) {
+        unsigned char* sp = P.spare + (size_t)r * LC.state_bytes;
+        if (!keep || rfl(((const Hdr*)(sp + kOffHdr))->episode) != episode + 1u) {
+            __syncthreads();
+            Hot H2;
+            memset(&H2, 0, sizeof(H2));
+            Regs<FS, LS> R2;
+            init_replica(S, R2, H2, episode + 1u, false);   // log position and totals: patched at restart
+            hot_store(S, R2, H2);
+            __syncthreads();
+            image_store(lds, LC, sp, lane, R2);
+        }
+    }
 }
 
 // step kernels (step_kernel.h): the instances with the --train / notify_dest code paths
@@ -177,6 +206,7 @@ struct prisma_env {
     const void* k_step_mlp = nullptr;
     const void* k_reset = nullptr;
     float* d_mlp_rp = nullptr;           // interleaved DQN-buffer layers 2-4 (prisma_run, mode 4)
+    unsigned char* d_spare = nullptr;    // next-episode images (register engine with auto_reset)
     bool reset_done = false;
 };
 
@@ -816,6 +846,12 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
         prisma_destroy(e);
         return set_err(PRISMA_ERR_NOMEM, "hipMalloc failed");
     }
+    // fused runs with auto_reset continue into the next episode from a prebuilt image
+    // (engine_core.h spare_restart): one more state image per replica
+    if (L.auto_reset && !L.mem && !HIP_OK(hipMalloc(&e->d_spare, sb))) {
+        prisma_destroy(e);
+        return set_err(PRISMA_ERR_NOMEM, "hipMalloc of the spare images failed");
+    }
     if (!HIP_OK(hipMemcpy(e->d_topo, img.data(), L.topo_bytes, hipMemcpyHostToDevice)) ||
         !HIP_OK(hipMemcpy(e->d_lay, &L, sizeof(Layout), hipMemcpyHostToDevice)) ||
         !HIP_OK(hipMemset(e->d_log, 0, lb)) ||
@@ -852,6 +888,7 @@ static KParams base_params(prisma_env_t* e) {
     P.log = e->d_log;
     P.cnt_out = e->d_cnt;
     P.R = e->R;
+    P.spare = e->d_spare;
     return P;
 }
 
@@ -927,6 +964,10 @@ extern "C" int prisma_run(prisma_env_t* e, int32_t policy, const void* policy_da
     }
     P.max_hops = max_hops;
     int rc = launch(e, P.mode == 4 ? e->k_step_mlp : e->k_step, P, stream);
+    // with auto_reset (register engine) the step kernel already continued every replica whose
+    // episode ended into the next one; this launch refreshes the spare images it used, and
+    // starts the next episode of the replicas it could not continue (memory engine; a second
+    // episode end in one launch)
     return rc ? rc : auto_reset(e, stream);
 }
 
@@ -1025,5 +1066,6 @@ extern "C" void prisma_destroy(prisma_env_t* e) {
     if (e->d_cnt) (void)hipFree(e->d_cnt);
     if (e->d_lay) (void)hipFree(e->d_lay);
     if (e->d_mlp_rp) (void)hipFree(e->d_mlp_rp);
+    if (e->d_spare) (void)hipFree(e->d_spare);
     delete e;
 }

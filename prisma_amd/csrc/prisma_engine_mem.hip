@@ -473,7 +473,7 @@ __global__ void __launch_bounds__(64) prisma_mem_step_kernel(KParams P) {
 #ifndef PRISMA_MLP_B_MEM
 #define PRISMA_MLP_B_MEM kMlpAll
 #endif
-    event_loop<MLP, PRISMA_MLP_B_MEM>(P, S, R, r);
+    event_loop<MLP, PRISMA_MLP_B_MEM>(P, S, R, r, (uint32_t)P.max_hops);
     mem_stage(lds, P, r, lane, true);
 }
 

@@ -38,7 +38,7 @@ prisma_step_kernel_t(KParams P) {
     S.tun = TUN;
     S.ctrl = CTRL;
     if (TUN) S.ring = (uint32_t*)(P.state + (size_t)r * LC.state_bytes + LC.s_ring);   // HBM FIFOs
-    event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P, S, R, r);
+    event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P, S, R, r, (uint32_t)P.max_hops);
     stage_out(lds, P, r, lane, R);
 }
 

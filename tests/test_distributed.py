@@ -70,3 +70,40 @@ def test_gloo_world2_gather_equals_single_process(oracle_mod, total):
         assert p.exitcode == 0
     ref = replica_stats(_counters_for(0, total))
     assert np.array_equal(got, ref)
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, env_extra=None, timeout=180):
+    import subprocess
+    import sys
+    import time
+    env = dict(os.environ, **(env_extra or {}))
+    env.pop("WORLD_SIZE", None)
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=timeout, cwd=ROOT, env=env)
+    return p, time.monotonic() - t0
+
+
+def test_bench_launcher_rendezvous_gloo_world2():
+    """bench.py --gpus 2 spawns its own ranks; with --rendezvous-only over gloo they initialise,
+    all-gather their replica shards and rank 0 reports world size and the gathered count."""
+    import json
+    p, _ = _bench(["--gpus", "2", "--rendezvous-only", "--backend", "gloo", "--replicas", "100",
+                   "--rank-deadline", "120"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["world_size"] == 2 and d["replicas_gathered"] == 200 and d["per_rank_replicas"] == [100, 100]
+
+
+def test_bench_launcher_deadline_names_stalled_rank():
+    """A rank that hangs (here: before its process-group init, so rank 0 waits in the rendezvous)
+    makes the launcher terminate every rank at the deadline, name the stalled rank and exit 124."""
+    deadline = 25.0
+    p, wall = _bench(["--gpus", "2", "--rendezvous-only", "--backend", "gloo", "--rank-deadline", str(deadline)],
+                     env_extra={"PRISMA_BENCH_STALL_RANK": "1"})
+    assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
+    assert wall < deadline + 20.0
+    assert "rank 1 (last stage: started)" in p.stderr and "rank 0 (last stage: started)" in p.stderr

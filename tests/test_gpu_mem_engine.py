@@ -11,6 +11,7 @@ from prisma_amd.config import engine_params
 from prisma_amd.engine import PRISMA_ENGINE_MEMORY, PRISMA_ENGINE_REGISTER, PrismaEngine
 from prisma_amd.records import COUNTERS_DTYPE
 from prisma_amd.topology import DATA_DIR, Topology, sp_next_hop_table
+from parity_util import check_near_ties
 
 pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")]
@@ -30,7 +31,7 @@ def er256():
     return topo, table
 
 
-def run_both(oracle_mod, topo, params, R, H, policy, launches=1, replicas=None, mlp=False):
+def run_both(oracle_mod, topo, params, R, H, policy, launches=1, replicas=None, mlp=False, net_cpu=None):
     eng = PrismaEngine(topo, params, R)
     assert eng.engine_kind == MEM
     eng.reset(0)
@@ -53,6 +54,8 @@ def run_both(oracle_mod, topo, params, R, H, policy, launches=1, replicas=None, 
         got = eng.records(r, len(ref) - n, n, log_host=log)
         assert got.tobytes() == ref[len(ref) - n:].tobytes(), f"replica {r} records differ"
         assert_counters_equal(cnt[r], o.counters(), r)
+        if net_cpu is not None:                  # torch fp32 argmin except at genuine near-ties
+            check_near_ties(net_cpu, policy.cpu().numpy(), o, got)
     eng.close()
     return cnt
 
@@ -162,7 +165,8 @@ def test_mem_dqn_buffer_parity(oracle_mod):
     topo = Topology.example("geant")
     w = StackedQNet(topo, "buffer", seed=21).pack()
     params = engine_params(topo, sim_time_s=10.0, ping_as_obs=0, replica_base=3, engine=MEM)
-    run_both(oracle_mod, topo, params, 3, 1500, w, launches=2, mlp=True)
+    run_both(oracle_mod, topo, params, 3, 1500, w, launches=2, mlp=True,
+             net_cpu=StackedQNet(topo, "buffer", seed=21, device="cpu"))
 
 
 # ---- BASELINE config 5: ER-256 ---------------------------------------------------------
@@ -196,7 +200,8 @@ def test_er256_dqn_buffer_parity(oracle_mod):
     topo, _ = er256()
     w = StackedQNet(topo, "buffer", seed=5).pack()
     params = engine_params(topo, sim_time_s=60.0, ping_as_obs=0, replica_base=1000)
-    run_both(oracle_mod, topo, params, 2, 2000, w, launches=2, mlp=True)
+    run_both(oracle_mod, topo, params, 2, 2000, w, launches=2, mlp=True,
+             net_cpu=StackedQNet(topo, "buffer", seed=5, device="cpu"))
 
 
 def test_er256_full_size_properties(oracle_mod):

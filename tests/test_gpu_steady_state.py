@@ -1,0 +1,106 @@
+"""Steady-state parity: every BASELINE workload compared with the CPU oracle record by record and
+counter by counter, after every launch, well past the flow-start transient.
+
+Flows start at 0.0001 + U(0, 1) s (/root/reference/prisma/ns3/sim.cc:610-630), so the first
+simulated second is a transient: flows still starting, FIFOs filling. These runs go on until all
+flows are active, FIFOs sit at their DropTail limit (point-to-point-net-device.cc:595-666), the
+ping windows are full, the uid / FIFO ring / ping round indices have wrapped and the clock is past
+2^32 ns; the headline workload runs a whole 60-s episode, its end and the auto-reset into episode 1
+(main.py:111-114's episode loop).
+
+Each test prints "compared up to t = ... s" for its workload. The DQN-buffer workloads also check
+every in-kernel decision against the fp32 torch model (parity_util.check_near_ties).
+"""
+import numpy as np
+import pytest
+import torch
+
+from parity_util import compare_steady
+from prisma_amd.config import engine_params
+from prisma_amd.engine import PrismaEngine
+from prisma_amd.topology import DATA_DIR, Topology
+
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")]
+
+
+def _buffer_net(topo, seed):
+    from prisma_amd.policies import StackedQNet
+    net = StackedQNet(topo, "buffer", seed=seed, device="cpu")
+    return net, net.pack().numpy()
+
+
+def test_config2_headline_full_episode_and_auto_reset(oracle_mod):
+    """Config 2 (the headline): Abilene TM0 lf 1.0, DQ-routing greedy table from the bench's
+    random-init weights (seed 1234), pingAsObs=1, simTime 60 s, auto-reset: a whole episode, its
+    end inside a launch (the replicas continue into episode 1 in the same launch) and 5 s of
+    episode 1, on 2 replicas."""
+    from prisma_amd.policies import StackedQNet
+    topo = Topology.example("abilene", 0, 1.0)
+    table = StackedQNet(topo, "routing", seed=1234, device="cpu").argmin_table().numpy()
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=1, auto_reset=1, seed=100, replica_base=17,
+                           log_capacity=65536)
+    eng = PrismaEngine(topo, params, 2)
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("table", table), t_target_s=65.0,
+                         hops_per_launch=16384, min_episode=1, label="config 2 abilene dq_routing")
+    eng.close()
+    assert out["t_compared_s"] >= 65.0 and min(out["episodes"]) >= 1
+    # the episode end happened inside a launch and the replicas continued into episode 1 there:
+    # every launch executed its whole hop budget (no work lost at the boundary)
+    assert out["short_launches"] == 0
+
+
+@pytest.mark.parametrize("ping", [0, 1])
+@pytest.mark.parametrize("lf", [0.5, 1.0, 2.0])
+def test_config4_geant_dqn_buffer_steady(oracle_mod, lf, ping):
+    """Config 4: GEANT TM0, in-kernel DQN-buffer, 15 s of simulated time on 2 replicas."""
+    topo = Topology.example("geant", 0, lf)
+    net, w = _buffer_net(topo, seed=41 + int(lf * 4))
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=ping, seed=100, replica_base=2048 + int(lf * 8),
+                           log_capacity=65536)
+    eng = PrismaEngine(topo, params, 2)
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("mlp", w), t_target_s=15.0, hops_per_launch=16384,
+                         net_cpu=net, label=f"config 4 geant lf {lf} pingAsObs {ping}")
+    eng.close()
+    assert out["t_compared_s"] >= 15.0 and out["mlp_decisions"] > 10000
+
+
+def test_config3_abilene_on_geant_dqn_buffer_steady(oracle_mod):
+    """Config 3: the Abilene overlay tunnelled over GEANT, DQN-buffer, pingAsObs=1, 15 s."""
+    topo = Topology.example("abilene_on_geant", 0, 1.0)
+    net, w = _buffer_net(topo, seed=7)
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=1, seed=100, replica_base=4000, log_capacity=65536)
+    eng = PrismaEngine(topo, params, 2)
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("mlp", w), t_target_s=15.0, hops_per_launch=16384,
+                         net_cpu=net, label="config 3 abilene-on-geant dqn_buffer")
+    eng.close()
+    assert out["t_compared_s"] >= 15.0 and out["mlp_decisions"] > 5000
+
+
+def test_config5_er256_dqn_buffer_steady(oracle_mod):
+    """Config 5: ER-256 on the memory-resident engine, DQN-buffer, pingAsObs=1, 3 s on 1 replica."""
+    topo = Topology.example("er256")
+    net, w = _buffer_net(topo, seed=5)
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=1, seed=100, replica_base=8191, log_capacity=65536)
+    eng = PrismaEngine(topo, params, 1)
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("mlp", w), t_target_s=3.0, hops_per_launch=16384,
+                         net_cpu=net, label="config 5 er256 dqn_buffer")
+    eng.close()
+    assert out["t_compared_s"] >= 3.0
+
+
+def test_config5_er256_sp_table_steady(oracle_mod):
+    """Config 5's graph with the SP table (the memory engine's table path), 3 s on 1 replica."""
+    topo = Topology.example("er256")
+    table = np.load(f"{DATA_DIR}/er256/sp_next_hop_table.npy")
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=0, seed=100, replica_base=3, log_capacity=65536)
+    eng = PrismaEngine(topo, params, 1)
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("table", table), t_target_s=3.0, hops_per_launch=16384,
+                         label="config 5 er256 sp")
+    eng.close()
+    assert out["t_compared_s"] >= 3.0
