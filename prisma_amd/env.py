@@ -113,7 +113,8 @@ class VecRoutingEnv:
         """Reward, done and info of the current notifications, from their decision records (the
         record of a data notification is the replica's last one, written when it was notified)."""
         R = self.R
-        dec = self._dec_counts()
+        cf = self._counter_fields()
+        dec = cf["dec_count"]
         live = mask.to(torch.bool)
         control = live & (obs[:, 0] == 1000)
         data = live & ~control & (dec > 0)
@@ -125,7 +126,10 @@ class VecRoutingEnv:
         done = data & (rec["status"] == ST_DESTINATION)
         info = {"mask": mask, "node": node, "control": control,
                 "uid": torch.where(data, rec["uid"], torch.full_like(rec["uid"], -1)),
-                "prev": torch.where(has_prev, rec["prev"], torch.full_like(rec["prev"], -1))}
+                "prev": torch.where(has_prev, rec["prev"], torch.full_like(rec["prev"], -1)),
+                # the replica's clock at this notification (Agent.curr_time, forwarder.py:208) and
+                # its episode index: the trainer schedules syncs and signalling delays on them
+                "now_ns": cf["now_ns"], "episode": cf["episode"]}
         return reward, done, info
 
     def run(self, table: torch.Tensor, max_hops: int):
@@ -134,11 +138,19 @@ class VecRoutingEnv:
     def counters(self) -> np.ndarray:
         return self.engine.counters()
 
-    def _dec_counts(self) -> torch.Tensor:
-        words = self.engine.counters_tensor().view(torch.int32)      # [R, 36]
+    def _counter_fields(self) -> dict:
+        """dec_count, now_ns and episode of every replica (device int64 [R])."""
         from .records import COUNTERS_DTYPE
-        off = COUNTERS_DTYPE.fields["dec_count"][1] // 4
-        return words[:, off].to(torch.int64) & 0xFFFFFFFF
+        raw = self.engine.counters_tensor()                         # [R, 152] bytes
+        w32 = raw.view(torch.int32)
+        w64 = raw.view(torch.int64)
+        f = COUNTERS_DTYPE.fields
+        return {"dec_count": w32[:, f["dec_count"][1] // 4].to(torch.int64) & 0xFFFFFFFF,
+                "now_ns": w64[:, f["now_ns"][1] // 8].clone(),
+                "episode": w32[:, f["episode"][1] // 4].to(torch.int64) & 0xFFFFFFFF}
+
+    def _dec_counts(self) -> torch.Tensor:
+        return self._counter_fields()["dec_count"]
 
     def transitions(self) -> dict:
         """Replay transitions completed since the previous call (device tensors).
@@ -158,7 +170,8 @@ class VecRoutingEnv:
         empty = {k: torch.zeros((0,) + s, dtype=t, device=self.device) for k, s, t in
                  [("obs", (W,), torch.int32), ("action", (), torch.int32), ("reward", (), torch.float64),
                   ("next_obs", (W,), torch.int32), ("done", (), torch.bool), ("node", (), torch.int32),
-                  ("replica", (), torch.int32), ("uid", (), torch.int64), ("hop", (), torch.bool)]}
+                  ("replica", (), torch.int32), ("uid", (), torch.int64), ("hop", (), torch.bool),
+                  ("t_ns", (), torch.int64)]}
         if total == 0:
             return empty
         rep = torch.repeat_interleave(torch.arange(self.R, device=self.device), n)
@@ -196,6 +209,8 @@ class VecRoutingEnv:
             "uid": torch.cat([cur_f["uid"][hp], cur_f["uid"][dr]]).to(torch.int64),
             "hop": torch.cat([torch.ones(int(hp.sum()), dtype=torch.bool, device=self.device),
                               torch.zeros(int(dr.sum()), dtype=torch.bool, device=self.device)]),
+            # when the transition completed: the next notification (hop) or the drop (loss)
+            "t_ns": torch.cat([cur_f["t_ns"][hp], cur_f["t_ns"][dr]]).to(torch.int64),
         }
         return out
 

@@ -180,6 +180,7 @@ class Topology:
     tun_len: Optional[np.ndarray] = None           # [T] links crossed
     next_hop: Optional[np.ndarray] = None          # [N, N] routing (route_tables)
     dist: Optional[np.ndarray] = None              # [N, N] hop distance
+    tm_strings: Optional[np.ndarray] = None        # [N, N] the traffic matrix as given (trainer's auto sync step)
 
     @property
     def n_links(self) -> int:
@@ -332,7 +333,7 @@ class Topology:
                    name=name, load_factor=float(load_factor),
                    overlay_index=overlay_index, overlay_nodes=overlay_nodes, overlay_adj=oadj,
                    ov_row_ptr=ov_row_ptr, tun_src=tun_src, tun_dst=tun_dst, tun_link=tun_link,
-                   tun_len=tun_len, next_hop=hop, dist=dist)
+                   tun_len=tun_len, next_hop=hop, dist=dist, tm_strings=tm)
 
     @classmethod
     def from_files(cls, physical_adjacency: str, overlay_adjacency: str, map_overlay: str,

@@ -150,9 +150,10 @@ def test_training_loop_on_the_engine():
     from prisma_amd.env import VecRoutingEnv
     from prisma_amd.trainer import train
     env = VecRoutingEnv("abilene", n_replicas=256, sim_time_s=30.0, ping_as_obs=0)
-    tr = QRoutingTrainer(env.topo, "buffer", batch_size=64, buffer_size=4096, seed=0)
+    tr = QRoutingTrainer(env.topo, "buffer", batch_size=64, buffer_size=4096, seed=0, n_replicas=256,
+                         sync_step=0.05)
     w0 = tr.q.W2.detach().clone()
-    losses = train(env, tr, steps=200, train_every=4, sync_every=50)
+    losses = train(env, tr, steps=200, train_every=4)
     env.close()
     assert losses and np.all(np.isfinite(losses))
     assert int(tr.buffers.total.sum()) > 200 * 256 // 2
@@ -188,7 +189,7 @@ def test_nn_signaling_copies_follow_the_reference_rules():
     q0 = snap()
     pairs = [(u, i) for u in range(11) for i in range(int(topo.degrees[u]))]
     cp = {p: {"t": q0, "up": q0, "tmp": q0} for p in pairs}
-    counter = np.zeros(11, dtype=int)
+    counter = np.full(11, -1, dtype=int)                     # Agent.sync_counters start at -1 (forwarder.py:123)
     rng = np.random.default_rng(4)
     g = torch.Generator().manual_seed(1)
     for step in range(6):
@@ -254,7 +255,7 @@ def test_hop_transitions_wait_for_their_echo(kind):
     enters u's buffer when its packet's echo is back at u (loss transitions at once); a
     "target" transition carries the next node's online-network target."""
     topo = Topology.example("abilene")
-    tr = QRoutingTrainer(topo, "buffer", seed=6, device="cpu", signaling_type=kind, batch_size=4)
+    tr = QRoutingTrainer(topo, "buffer", seed=6, device="cpu", signaling_type=kind, batch_size=4, n_replicas=3)
     rng = np.random.default_rng(8)
     b = _hop_batch(topo, rng, 40)
     hop = b["hop"].numpy()
@@ -302,9 +303,241 @@ def test_training_loop_with_nn_signaling():
     env = VecRoutingEnv("abilene", n_replicas=64, sim_time_s=30.0, ping_as_obs=1, train=1, notify_dest=1,
                         signaling_type="NN", big_signaling=1, sync_step_s=0.05, big_signaling_bytes=1024)
     tr = QRoutingTrainer(env.topo, "buffer", batch_size=32, buffer_size=4096, seed=0, signaling_type="NN",
-                         nn_max_seg_index=1024 // 512 - 1)
-    losses = train(env, tr, steps=600, train_every=4, sync_every=20)
+                         big_signaling_size=1024, n_replicas=64, sync_step=0.05)
+    losses = train(env, tr, steps=600, train_every=4)
     env.close()
     assert losses and np.all(np.isfinite(losses))
     assert int(tr.buffers.total.sum()) > 0
     assert bool((tr.tgt_ver > 0).any())
+
+
+# ---- PrioritizedReplayBuffer (replay_buffer.py:393-534) ----------------------------------
+PRIO_GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "prio_replay_buffer.json")
+
+
+def test_prioritized_replay_matches_reference_fixture():
+    """Per-node prioritized rings against the states the reference's own PrioritizedReplayBuffer
+    reached on the same operation script (tests/golden/make_prio_replay_golden.py): priorities of
+    the stored slots (sum-tree leaves), the tree total (bit for bit: the same pairwise sums), max
+    priority, latest gradient steps, the per-action slot lists, and the importance weights of the
+    samples the reference drew (fed the same indices)."""
+    fx = json.load(open(PRIO_GOLDEN))
+    deg, size, W = fx["degrees"], fx["size"], fx["obs_width"]
+    N = len(deg)
+    buf = ReplayBuffers(N, size, W, device="cpu", prioritized=True, max_deg=max(deg), alpha=fx["alpha"])
+    n_samples = 0
+    for op, rec in zip(fx["ops"], fx["trace"]):
+        u = op["node"]
+        if op["op"] == "add":
+            buf.add({"node": torch.tensor([u]), "obs": torch.tensor([op["obs"]], dtype=torch.int32),
+                     "next_obs": torch.tensor([op["next_obs"]], dtype=torch.int32),
+                     "action": torch.tensor([op["action"]]), "reward": torch.tensor([op["reward"]]),
+                     "done": torch.tensor([op["done"]]), "prio": torch.tensor([op["prio"]], dtype=torch.float64)})
+        elif op["op"] == "grad":
+            buf.gradient_step(u, op["action"], op["step"])
+        elif not rec.get("skipped"):
+            B = len(rec["idx"])
+            idx = torch.zeros((N, B), dtype=torch.int64)
+            idx[u] = torch.tensor(rec["idx"])
+            smp = buf.sample_full(B, idx=idx)
+            assert smp["obs"][u, :, 0].tolist() == rec["tags"]
+            assert smp["weights"][u].tolist() == rec["weights"]
+            n_samples += 1
+        st = rec["state"]
+        n = st["len"]
+        assert int(buf.count[u]) == n and int(buf.next_idx[u]) == st["next_idx"]
+        assert int(buf.total[u]) == st["total_samples"]
+        assert buf.obs[u, :n, 0].tolist() == st["tags"]
+        assert buf.prio[u, :n].tolist() == st["prio"] == st["prio_min"]
+        assert float(buf.tree_sum()[u]) == st["tree_sum"]
+        assert float(buf.max_prio[u]) == st["max_priority"]
+        assert buf.latest[u, :deg[u]].tolist() == st["latest_gradient_step"]
+        for a in range(deg[u]):
+            assert set(torch.nonzero(buf.member[u, a]).squeeze(1).tolist()) == set(st["neighbors_idx"][a])
+    assert n_samples >= 10
+
+
+def test_prioritized_batch_add_equals_one_by_one():
+    """A batch add (several nodes, overflowing rings) equals the same transitions added one by one."""
+    rng = np.random.default_rng(3)
+    N, size, W, D = 4, 5, 4, 3
+    n = 37
+    tr = {"node": torch.from_numpy(rng.integers(0, N, n)), "obs": torch.from_numpy(rng.integers(0, 99, (n, W))).int(),
+          "next_obs": torch.from_numpy(rng.integers(0, 99, (n, W))).int(),
+          "action": torch.from_numpy(rng.integers(0, D, n)), "reward": torch.from_numpy(rng.random(n)),
+          "done": torch.from_numpy(rng.random(n) < 0.3), "prio": torch.from_numpy(rng.integers(1, 5, n)).double()}
+    a = ReplayBuffers(N, size, W, device="cpu", prioritized=True, max_deg=D)
+    b = ReplayBuffers(N, size, W, device="cpu", prioritized=True, max_deg=D)
+    a.gradient_step(1, 2, 3)
+    b.gradient_step(1, 2, 3)
+    a.add(tr)
+    for i in range(n):
+        b.add({k: t[i:i + 1] for k, t in tr.items()})
+    for f in ("obs", "action", "count", "next_idx", "total", "prio", "orig", "member", "max_prio"):
+        assert torch.equal(getattr(a, f), getattr(b, f)), f
+
+
+def test_prioritized_loss_is_importance_weighted():
+    """learner.py:179: mean(weights * huber) per node, weights from the prioritized buffer."""
+    topo = Topology.example("abilene")
+    tr = QRoutingTrainer(topo, "buffer", seed=5, device="cpu", batch_size=8, lr=1e-3, prioritized_replay=True)
+    rng = np.random.default_rng(6)
+    n = 200
+    node = torch.from_numpy(rng.integers(0, 11, n))
+    obs = torch.from_numpy(rng.integers(0, 16000, (n, topo.obs_width)).astype(np.int32))
+    obs[:, 0] = torch.from_numpy(rng.integers(0, 11, n).astype(np.int32))
+    act = torch.tensor([int(rng.integers(0, topo.degrees[u])) for u in node.tolist()])
+    tr.observe({"node": node, "obs": obs, "next_obs": obs.clone(), "action": act,
+                "reward": torch.full((n,), 0.01), "done": torch.ones(n, dtype=torch.bool)})
+    for u in range(11):                                     # newer steps for action 0: priorities below 1
+        tr.buffers.gradient_step(u, 0, 4)
+    g = torch.Generator().manual_seed(9)
+    tr.gen = torch.Generator().manual_seed(9)
+    s = tr.buffers.sample_full(8, g)
+    per = tr.train_step()
+    N, B = 11, 8
+    q = StackedQNet_copy = None
+    assert per is not None and torch.isfinite(per[~torch.isnan(per)]).all()
+    w = s["weights"]
+    assert bool((w[s["action"] == 0] < 1.0).any()) and bool((w[s["action"] != 0] >= 1.0).all())
+
+
+# ---- signalingSim=0: the agents' own signalling delays (forwarder.py:94-108, trainer.py) -----
+class _RefAgents:
+    """A literal per-replica restatement of the reference's signalingSim=0 bookkeeping: one
+    upcoming-event list per node kept sorted by time (forwarder.py:434-442), released while its
+    head's time <= Agent.curr_time (forwarder.py:444-464), then the sync check (trainer.py:101-112,
+    155-171); target copies as version numbers."""
+
+    def __init__(self, topo, R, sync_step, small_delay, big_delay):
+        self.topo, self.R = topo, R
+        self.sync_step, self.small_delay, self.big_delay = sync_step, small_delay, big_delay
+        N = topo.n_nodes
+        self.upcoming = [[[] for _ in range(N)] for _ in range(R)]
+        self.counter = np.full((R, N), -1)
+        D = topo.max_deg
+        self.tgt = np.zeros((R, N, D), dtype=int)
+        self.up = np.zeros((R, N, D), dtype=int)
+        self.tmp = np.zeros((R, N, D), dtype=int)
+        self.buffers = [[] for _ in range(N)]
+        self.version = 0
+
+    def push(self, r, u, item):
+        item["seq"] = self.seq = getattr(self, "seq", 0) + 1
+        self.upcoming[r][u].append(item)
+        self.upcoming[r][u].sort(key=lambda e: e["time"])
+
+    def step(self, clock):
+        released = []
+        for r in range(self.R):
+            for u in range(self.topo.n_nodes):
+                q = self.upcoming[r][u]
+                while q and q[0]["time"] <= clock[r]:
+                    e = q.pop(0)
+                    if "tag" in e:
+                        released.append((e["time"], e["seq"], u, e["tag"]))
+                    else:
+                        self.tgt[r, u, e["i"]] = self.up[r, u, e["i"]]
+        # the replicas are separate simulations sharing the per-node buffers: one step's releases
+        # enter them in time order across replicas (the trainer's choice; one simulation has no
+        # such merge)
+        for _, _, u, tg in sorted(released):
+            self.buffers[u].append(tg)
+        due = [(r, u) for r in range(self.R) for u in range(self.topo.n_nodes)
+               if self.topo.degrees[u] > 0 and clock[r] > (self.counter[r, u] + 1) * self.sync_step]
+        if due:
+            self.version += 1
+        for r, u in due:
+            for i in range(int(self.topo.degrees[u])):
+                self.tmp[r, u, i] = self.up[r, u, i]
+                self.up[r, u, i] = self.version
+                self.push(r, u, {"time": clock[r] + self.big_delay[u], "i": i})
+            self.counter[r, u] += 1
+
+
+def test_signaling_sim0_nn_queues_follow_the_reference():
+    """signalingSim=0 with "NN": hop transitions reach u's buffer small_signaling_delay(v) after
+    their notification, every sync queues the neighbours' NNs for big_signaling_delay(u), and the
+    target copies follow, per replica, against the literal restatement above."""
+    topo = Topology.example("abilene")
+    R = 3
+    tr = QRoutingTrainer(topo, "buffer", seed=2, device="cpu", signaling_type="NN", signaling_sim=0,
+                         n_replicas=R, sync_step=0.3, batch_size=4)
+    # forwarder.py:94-108: sizes and delays
+    for u in range(11):
+        d = int(topo.degrees[u])
+        assert tr.small_size[u] == 64 + 8 + 8 * (d + 1)
+        assert tr.nn_size[u] == 32 * sum(int(p[u].numel()) for p in (tr.q.W1[:, :topo.n_overlay], tr.q.b1)) \
+            + 32 * ((d * 32 + 32) + (64 * 64 + 64) * 2 + 64 * d + d)
+        assert tr.small_delay[u] == tr.small_size[u] / 500000 + 0.001
+        assert tr.big_delay[u] == tr.nn_size[u] / 500000 + 0.001
+    ref = _RefAgents(topo, R, 0.3, tr.small_delay, tr.big_delay)
+    rng = np.random.default_rng(11)
+    clock = np.zeros(R)
+    tag = 0
+    for step in range(120):
+        clock = clock + rng.random(R) * 0.03
+        n = int(rng.integers(0, 6))
+        node = rng.integers(0, 11, n)
+        act = np.array([int(rng.integers(0, topo.degrees[u])) for u in node], dtype=np.int64)
+        rep = rng.integers(0, R, n)
+        t_ns = np.array([int((clock[r] - rng.random() * 0.01) * 1e9) for r in rep], dtype=np.int64)
+        hop = rng.random(n) < 0.8
+        obs = np.zeros((n, topo.obs_width), dtype=np.int32)
+        obs[:, 0] = np.arange(tag, tag + n)
+        for j in range(n):
+            v = topo.neighbors(int(node[j]))[act[j]]
+            if hop[j]:
+                ref.push(int(rep[j]), int(node[j]), {"time": t_ns[j] / 1e9 + tr.small_delay[v], "tag": tag + j})
+            else:
+                ref.buffers[int(node[j])].append(tag + j)
+        tag += n
+        batch = {"node": torch.from_numpy(node).int(), "obs": torch.from_numpy(obs), "next_obs": torch.from_numpy(obs),
+                 "action": torch.from_numpy(act).int(), "reward": torch.full((n,), 0.01, dtype=torch.float64),
+                 "done": torch.zeros(n, dtype=torch.bool), "replica": torch.from_numpy(rep).int(),
+                 "uid": torch.arange(n, dtype=torch.int64), "hop": torch.from_numpy(hop), "t_ns": torch.from_numpy(t_ns)}
+        # the reference releases transitions pushed in an earlier round only: push first, then step
+        tr.advance_clock(torch.from_numpy((clock * 1e9).astype(np.int64)))
+        tr.on_step(torch.zeros((R, topo.obs_width), dtype=torch.int32), {"transitions": batch})
+        ref.step(clock)
+        for u in range(11):
+            cnt = int(tr.buffers.count[u])
+            got = tr.buffers.obs[u, :cnt, 0].tolist()
+            assert got == (ref.buffers[u][-cnt:] if cnt else []), (step, u, got, ref.buffers[u])
+        valid = np.arange(topo.max_deg)[None, None, :] < topo.degrees[None, :, None]
+        assert np.array_equal(tr.tgt_ver * valid, ref.tgt) and np.array_equal(tr.up_ver * valid, ref.up), step
+    assert tr.big_pkts > 0 and tr.small_pkts > 0 and bool((tr.tgt_ver > 0).any())
+
+
+def test_compute_sync_step_matches_trainer_formula():
+    """trainer.py:114-134: nn_size / (sum(TM) * ratio - pkts_per_s * small_signaling_pkt_size)."""
+    topo = Topology.example("abilene")
+    tr = QRoutingTrainer(topo, "buffer", seed=0, device="cpu", signaling_type="NN", sync_step=-1, sync_ratio=0.1)
+    from prisma_amd.trainer import convert_bps_to_data_rate
+    data = sum(convert_bps_to_data_rate(x) for x in np.asarray(topo.tm_strings, dtype=object).ravel())
+    for u in range(11):
+        want = tr.nn_size[u] / (data * 0.1 - data / (512 * 8) * (64 + 8 + 8 * (topo.degrees[u] + 1)))
+        assert abs(tr.sync_step[u] - want) <= 1e-12 * abs(want)
+    assert convert_bps_to_data_rate("12.5Kbps") == 12500.0 and convert_bps_to_data_rate("3Mbps") == 3e6
+
+
+def test_echo_releases_only_the_first_queued_match_and_new_episode_drops_the_queue():
+    """forwarder.py:477-490 pops ONE element per echo (the first in time order); a replica that
+    starts a new episode forgets its queued transitions (agent.py:141-145)."""
+    topo = Topology.example("abilene")
+    tr = QRoutingTrainer(topo, "buffer", seed=6, device="cpu", signaling_type="NN", batch_size=4, n_replicas=2)
+    obs = torch.zeros((3, topo.obs_width), dtype=torch.int32)
+    obs[:, 0] = torch.tensor([7, 8, 9], dtype=torch.int32)
+    b = {"node": torch.tensor([3, 3, 3], dtype=torch.int32), "obs": obs, "next_obs": obs,
+         "action": torch.tensor([0, 0, 0], dtype=torch.int32), "reward": torch.zeros(3, dtype=torch.float64),
+         "done": torch.zeros(3, dtype=torch.bool), "replica": torch.tensor([0, 0, 1], dtype=torch.int32),
+         "uid": torch.tensor([5, 5, 5]), "hop": torch.ones(3, dtype=torch.bool),
+         "t_ns": torch.tensor([2_000_000, 1_000_000, 1_000_000])}
+    tr.observe(b)
+    eo = torch.zeros((2, topo.obs_width), dtype=torch.int32)
+    eo[0, 0], eo[0, 1] = 1000, 5
+    tr.on_control(eo, {"control": torch.tensor([True, False]), "node": torch.tensor([3, -1], dtype=torch.int32)})
+    assert tr.buffers.obs[3, :int(tr.buffers.count[3]), 0].tolist() == [8]      # the earlier of the two
+    tr.advance_clock(torch.tensor([5_000_000, 5_000_000]), torch.tensor([0, 1]))  # replica 1: next episode
+    assert tr._pend_key.numel() == 1 and int(tr._pend["replica"][0]) == 0
+    assert tr.sync_counter[1].max() == -1
