@@ -171,7 +171,7 @@ class OracleSim:
         cfg.signaling_type = int(params.get("signaling_type", 0))
         cfg.big_signaling = int(params.get("big_signaling", 0))
         cfg.sync_step_s = float(params.get("sync_step_s", 1.0))
-        cfg.big_signaling_bytes = int(params.get("big_signaling_bytes", 35328))
+        cfg.big_signaling_bytes = int(params.get("big_signaling_bytes", 512))
         self._cfg = cfg
         self.W = topo.obs_width
         self.rec_dtype = record_dtype(self.W)

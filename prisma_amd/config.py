@@ -74,7 +74,7 @@ def engine_params(topo: Topology, *, sim_time_s: float = 60.0, seed: int = 100, 
                   auto_reset: int = 0, log_capacity: int = 8192, replica_base: int = 0,
                   loss_penalty: Optional[float] = None, train: int = 0, notify_dest: int = 0,
                   engine: int = 0, signaling_type="ideal", big_signaling: int = 0, sync_step_s: float = 1.0,
-                  big_signaling_bytes: int = 35328) -> dict:
+                  big_signaling_bytes: int = DEFAULTS["bigSignalingSize"]) -> dict:
     """prisma_params_t as a dict (shared by the engine binding and the oracle).
 
     train=1 is the reference's --train: every data notification at a non-source
@@ -84,7 +84,8 @@ def engine_params(topo: Topology, *, sim_time_s: float = 60.0, seed: int = 100, 
     signaling_type ("ideal" / "NN" / "target" or 0 / 1 / 2) sets the echo's payload (sim.cc:373-392);
     big_signaling=1 is the simulator's --signaling with "NN" and --train: NN-weight segments of
     big_signaling_bytes every sync_step_s between overlay neighbours (sim.cc:634-647; run_ns3.py
-    passes signalingSim, sync_step and bigSignalingSize).  The simulator switches --signaling off
+    passes signalingSim, sync_step and bigSignalingSize, whose argument_parser.py:74 default, 512 B = one
+    segment per NN, is the default here too; sim.cc's own default is 35328).  The simulator switches --signaling off
     for the sp / opt agents and for "ideal" (sim.cc:374-376): the caller's part, as in run_ns3.py."""
     if log_capacity < 1024 or log_capacity > (1 << 22) or log_capacity & (log_capacity - 1):
         raise ValueError("log_capacity must be a power of two in [1024, 2^22]")

@@ -1808,23 +1808,27 @@ __device__ __forceinline__ void publish_counters(const Sim& S, const KParams& P,
 // same launch and spends the rest of its budget there.  The next episode's fresh image (LDS
 // part + register part) is built ahead of time by the reset kernel into P.spare, so the restart
 // is a copy: the LDS image and the registers are reloaded from it, and the log position and
-// the running totals carried over.  Built in place instead (init_replica's Philox draws inside
-// the loop, or an outer loop around the event loop, or an out-of-line call) the restart cost
-// the event loop its register allocation (scripts/asm_headline.sh: 24-60 VGPR spills).
-// Without a valid spare (two episode ends in one launch) the launch stops at the end as
-// before and the reset kernel after it starts the next episode.
+// the running totals carried over.  The step kernel then runs a second inlined copy of the
+// event loop (step_kernel.h).  Restarting inside the first loop instead -- its clock and
+// sequence numbers then get a second incoming value -- cost the hot loop ~20 VGPRs and 13 %
+// (A/B, profiles/r03a); so did Philox draws in the loop, an outer loop around it or an
+// out-of-line call (scripts/asm_headline.sh: 24-60 VGPR spills).  Without a valid spare (a
+// second episode end in one launch) the replica stops at the end and the reset kernel after
+// the launch starts its next episode.
 // ---------------------------------------------------------------------------
 template <int FS, int LS>
-__device__ __forceinline__ bool spare_restart(const KParams& P, Sim& S, Regs<FS, LS>& R, Hot& H, int r,
-                                              uint32_t& max_hops) {
-    if (!P.spare || H.error || H.hops_launch >= max_hops) return false;
+__device__ __forceinline__ bool spare_restart(const KParams& P, Sim& S, Regs<FS, LS>& R, int r, uint32_t done,
+                                              uint32_t& budget) {
     CLayout& LC = *(CLayout*)P.lay;
+    if (!P.spare || !LC.auto_reset || (P.mode != 2 && P.mode != 4) || done >= budget) return false;
+    if (!u_ld32(&S.h->over) || u_ld32(&S.h->error)) return false;
     const unsigned char* sp = P.spare + (size_t)r * LC.state_bytes;
-    if (rfl(((const Hdr*)(sp + kOffHdr))->episode) != H.episode + 1u) return false;
+    if (rfl(((const Hdr*)(sp + kOffHdr))->episode) != u_ld32(&S.h->episode) + 1u) return false;
     const int lane = S.lane;
-    const uint32_t dec = H.dec;
-    const uint64_t ht = (uint64_t)u_ld64((const int64_t*)&S.h->hops_total) + H.hops_launch;
-    const uint64_t et = (uint64_t)u_ld64((const int64_t*)&S.h->events_total) + H.ev_launch;
+    // carried over: the log position and the running totals (hot_store has added this launch's)
+    const uint32_t dec = u_ld32(&S.h->dec_count);
+    const uint64_t ht = (uint64_t)u_ld64((const int64_t*)&S.h->hops_total);
+    const uint64_t et = (uint64_t)u_ld64((const int64_t*)&S.h->events_total);
     __syncthreads();
     const uint4* s4 = (const uint4*)sp;
     uint4* d4 = (uint4*)S.base;
@@ -1836,13 +1840,11 @@ __device__ __forceinline__ bool spare_restart(const KParams& P, Sim& S, Regs<FS,
         S.c->dec_count = dec; S.c->hops_total = ht; S.c->events_total = et;
     }
     __syncthreads();
-    max_hops -= H.hops_launch;
-    hot_load(S, H);                                      // the new episode: clock 0, nothing pending
-    flow_min_refresh(S, R, H);
+    budget -= done;
     return true;
 }
 template <class RS>
-__device__ __forceinline__ bool spare_restart(const KParams&, Sim&, RS&, Hot&, int, uint32_t&) { return false; }
+__device__ __forceinline__ bool spare_restart(const KParams&, Sim&, RS&, int, uint32_t, uint32_t&) { return false; }
 
 // ---------------------------------------------------------------------------
 // the event loop of one launch (both engines): finish the pending decision,
@@ -1908,8 +1910,6 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
         if (bt >= L.t_end()) {                           // Simulator::Stop(simTime) (sim.cc:703)
             lazy_resolve(S, R, H, true);                 // here, not after the loop: there it costs registers
             H.over = 1;
-            // fused run with auto_reset: the next episode starts here, from its prebuilt image
-            if (table_mode && spare_restart(P, S, R, H, r, max_hops)) continue;
             H.stop = 1;
             break;
         }

@@ -9,7 +9,11 @@
 // VGPRs) for small replicas so 4096 of them are resident on 256 CUs at
 // once, 2 (<= 256) up to 512 flows x 128 links
 template <int FS, int LS> struct StepOcc {
+#ifdef PRISMA_DEV_WAVES
+    static constexpr int waves = PRISMA_DEV_WAVES;     // register-allocation experiments only
+#else
     static constexpr int waves = (FS <= 2 && LS == 1) ? 4 : (LS <= 2 ? 2 : 1);
+#endif
 #ifndef PRISMA_MLP_B_WIDE
 #define PRISMA_MLP_B_WIDE 8
 #endif
@@ -38,7 +42,21 @@ prisma_step_kernel_t(KParams P) {
     S.tun = TUN;
     S.ctrl = CTRL;
     if (TUN) S.ring = (uint32_t*)(P.state + (size_t)r * LC.state_bytes + LC.s_ring);   // HBM FIFOs
-    event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P, S, R, r, (uint32_t)P.max_hops);
+    uint32_t budget = (uint32_t)P.max_hops;
+    const uint32_t done = event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P, S, R, r, budget);
+    // an episode ended with hop budget left (fused run with auto_reset): the next episode from
+    // its prebuilt image, in a second inlined copy of the event loop.  A restart inside the first
+    // loop would give its clock and sequence numbers a second incoming value each iteration and
+    // cost the hot loop ~20 VGPRs (scripts/asm_headline.sh); this copy runs at most once per
+    // launch, after which a second episode end stops the replica as before.
+    if (P.spare && done < budget) {
+        // the kernel arguments are read again here rather than kept in SGPRs across the first loop
+        const KParams* kp = (const KParams*)__builtin_amdgcn_kernarg_segment_ptr();
+        asm volatile("" : "+s"(kp));
+        const KParams P2 = *kp;
+        if (spare_restart(P2, S, R, r, done, budget))
+            event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P2, S, R, r, budget);
+    }
     stage_out(lds, P, r, lane, R);
 }
 

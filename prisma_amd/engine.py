@@ -54,7 +54,8 @@ class _Params(C.Structure):
     ]
 
 
-_PARAM_DEFAULTS = dict(engine=0, signaling_type=0, big_signaling=0, sync_step_s=1.0, big_signaling_bytes=35328)
+# the defaults of config.engine_params (argument_parser.py:72-74, 86; bigSignalingSize 512)
+_PARAM_DEFAULTS = dict(engine=0, signaling_type=0, big_signaling=0, sync_step_s=1.0, big_signaling_bytes=512)
 
 
 class _LogView(C.Structure):

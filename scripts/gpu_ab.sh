@@ -1,0 +1,22 @@
+#!/bin/bash
+# A/B of the working tree's library against prebuilt variants (prisma_amd/_ablate/libprisma_amd_<name>.so),
+# alternating on one box, over several bench configurations.  Each line: lib, config, Mhops/s, kernel ms,
+# hops per launch.  Usage: bash scripts/gpu_ab.sh <tag> "<variants>" [steps warmup]
+TAG=${1:-x}
+VARS=${2:-base}
+STEPS=${3:-20}
+WARM=${4:-5}
+mkdir -p gpurun_out
+CONFIGS=("headline|" "geant_dqn|--topology geant --policy dqn_buffer --ping-as-obs 0 --replicas 2048"
+         "aog_dqn|--topology abilene_on_geant --policy dqn_buffer")
+for i in 1 2; do
+  for c in "${CONFIGS[@]}"; do
+    name=${c%%|*}; args=${c#*|}
+    for lib in $VARS new; do
+      if [ $lib = new ]; then unset PRISMA_LIB; else export PRISMA_LIB=$PWD/prisma_amd/_ablate/libprisma_amd_$lib.so; fi
+      out=gpurun_out/ab_${TAG}_${name}_${lib}_$i.json
+      timeout -k 10 200 python bench.py --cpu-baseline 0 --steps $STEPS --warmup $WARM $args > $out || exit 1
+      python -c "import json; d=json.load(open('$out')); print('$lib', '$name', round(d['value']/1e6,1), 'Mhops/s', round(d['roofline']['kernel_ms'],2), 'ms', 'hops/launch', d['roofline']['hops_per_launch'])"
+    done
+  done
+done

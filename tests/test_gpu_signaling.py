@@ -18,7 +18,9 @@ pytestmark = [pytest.mark.gpu,
 
 
 def sig_params(topo, **kw):
-    base = dict(sim_time_s=4.0, ping_as_obs=1, train=1, signaling_type="NN", big_signaling=1, replica_base=3)
+    # sim.cc's default NN size (69 segments per NN); engine_params defaults to the Python CLI's 512
+    base = dict(sim_time_s=4.0, ping_as_obs=1, train=1, signaling_type="NN", big_signaling=1, replica_base=3,
+                big_signaling_bytes=35328)
     base.update(kw)
     return engine_params(topo, **base)
 

@@ -71,7 +71,7 @@ def test_info_renderer_matches_oracle(oracle_mod):
 
 
 @pytest.mark.parametrize("sig", [dict(), dict(signaling_type="target"),
-                                 dict(signaling_type="NN", big_signaling=1)])
+                                 dict(signaling_type="NN", big_signaling=1, big_signaling_bytes=35328)])
 def test_control_info_renderer_matches_oracle(oracle_mod, sig):
     topo = Topology.example("abilene")
     params = engine_params(topo, sim_time_s=2.0, ping_as_obs=1, notify_dest=1, train=1, **sig)

@@ -14,7 +14,8 @@ P_NS = 14492754                            # 4096 / (35328 * 8 / 1.0f) s, rounde
 
 
 def big_params(topo, **kw):
-    base = dict(sim_time_s=2.0, ping_as_obs=1, train=1, signaling_type="NN", big_signaling=1)
+    # sim.cc's NN size (69 segments per NN; engine_params defaults to the Python CLI's 512 B)
+    base = dict(sim_time_s=2.0, ping_as_obs=1, train=1, signaling_type="NN", big_signaling=1, big_signaling_bytes=35328)
     base.update(kw)
     return engine_params(topo, **base)
 
