@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--rendezvous-only", action="store_true",
                    help="ranks only initialise torch.distributed and all-gather their replica counts (no GPU "
                         "work unless the backend is nccl): a check of the N-rank plumbing")
+    p.add_argument("--force-dist", action="store_true",
+                   help="initialise torch.distributed and run the collectives even with one rank (exercises "
+                        "RCCL init and the all-gather on a one-GPU box)")
     p.add_argument("--backend", default=None, choices=["nccl", "gloo"],
                    help="process-group backend (default: nccl = RCCL; gloo with --same-device)")
     a = p.parse_args()
@@ -275,6 +278,13 @@ def rendezvous_only(args, world: int, rank: int) -> None:
     import torch.distributed as dist
     from prisma_amd.dist import shard
     backend = args.backend or ("gloo" if args.same_device else "nccl")
+    for k, v in (("MASTER_ADDR", "127.0.0.1"), ("RANK", str(rank)), ("WORLD_SIZE", str(world))):
+        os.environ.setdefault(k, v)
+    if "MASTER_PORT" not in os.environ:                     # one rank without the launcher
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+        sk.close()
     if backend == "nccl":
         dev = torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0")))
         torch.cuda.set_device(dev)
@@ -316,8 +326,16 @@ def main():
     backend = args.backend or ("gloo" if args.same_device else "nccl")
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
-    if world > 1:
+    use_dist = world > 1 or args.force_dist
+    if use_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:                 # a 1-rank group of its own (--force-dist)
+            sk = socket.socket()
+            sk.bind(("127.0.0.1", 0))
+            os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
+            sk.close()
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -359,7 +377,7 @@ def main():
     c0 = eng.counters()
     stream = torch.cuda.current_stream()
     evs = []
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -372,12 +390,12 @@ def main():
         e1.record(stream)
         evs.append((e0, e1))
     torch.cuda.synchronize()
-    if world > 1:
+    if use_dist:
         dist.barrier()
     t1 = time.perf_counter()
     report_stage("timed")
     elapsed = t1 - t0
-    if world > 1:
+    if use_dist:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
@@ -388,7 +406,7 @@ def main():
     errors = int(c1["error"].max())
     stats = gather_replica_stats(c1, world, device=coll_dev)   # RCCL all-gather (outside the timed region)
     per_rank = [hops_local]
-    if world > 1:
+    if use_dist:
         ht = torch.zeros(world, dtype=torch.int64, device=coll_dev)
         ht[rank] = hops_local
         dist.all_reduce(ht)
@@ -440,7 +458,7 @@ def main():
                 "issue": issue_roofline(args.topology, args.replicas, args.hops, bid),
             },
             "errors": errors,
-            "dist": {"world_size": dist.get_world_size() if world > 1 else 1, "backend": backend if world > 1 else None,
+            "dist": {"world_size": dist.get_world_size() if use_dist else 1, "backend": backend if use_dist else None,
                      "replicas_gathered": int(stats["stats"].shape[0])},
             "episodes_completed": stats["episodes_completed"],
             "replicas_total": int(stats["stats"].shape[0]),
@@ -451,7 +469,7 @@ def main():
                                                   policy().cpu().numpy(), args.cpu_hops, args.cpu_hops_1core)
         print(json.dumps(result), flush=True)
     eng.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
     report_stage("done")
 

@@ -40,9 +40,10 @@ def gather_replica_stats(counters: np.ndarray, world: int, device=None) -> dict:
     "delivered": int, "lost": int}.
     """
     import torch
+    import torch.distributed as dist
     local = torch.from_numpy(replica_stats(counters))
-    if world > 1:
-        import torch.distributed as dist
+    # the collective runs whenever a process group is up (also a 1-rank group: bench.py --force-dist)
+    if world > 1 or (dist.is_available() and dist.is_initialized()):
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" \
                 else torch.device("cpu")

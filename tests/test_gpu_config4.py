@@ -155,3 +155,25 @@ def test_bench_two_ranks_same_device():
     assert d["errors"] == 0 and d["n_gpus"] == 1
     assert abs(d["value"] - sum(d["per_rank_hops_s"])) <= 1e-6 * d["value"]
     assert d["roofline"]["build_id"]
+
+
+@pytest.mark.parametrize("mode", ["rendezvous", "bench"])
+def test_bench_rccl_one_rank_group(mode):
+    """The RCCL path on a one-GPU box: a one-rank nccl process group initialises (device-bound,
+    as bench.py's ranks do) and runs the bench's collectives -- the barriers, the max-over-ranks
+    all-reduce and the replica-statistics all-gather of prisma_amd/dist.py (--force-dist)."""
+    if mode == "rendezvous":
+        args = ["--rendezvous-only", "--backend", "nccl", "--replicas", "64"]
+    else:
+        args = ["--force-dist", "--backend", "nccl", "--steps", "2", "--warmup", "1", "--replicas", "128",
+                "--hops", "256", "--cpu-baseline", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=300, cwd=ROOT, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    if mode == "rendezvous":
+        assert d["backend"] == "nccl" and d["world_size"] == 1 and d["replicas_gathered"] == 64
+    else:
+        assert d["dist"] == {"world_size": 1, "backend": "nccl", "replicas_gathered": 128}
+        assert d["errors"] == 0 and d["replicas_total"] == 128
