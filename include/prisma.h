@@ -73,11 +73,12 @@ extern "C" {
 /* engine selection (prisma_params_t.engine) */
 #define PRISMA_ENGINE_AUTO     0   /* register-resident when the topology fits it */
 #define PRISMA_ENGINE_REGISTER 1   /* replica state in VGPRs + LDS: <= 255 nodes,
-                                      256 links / tunnels, 512 flows             */
+                                      256 links / tunnels / big-signalling
+                                      generators, 512 flows                      */
 #define PRISMA_ENGINE_MEMORY   2   /* replica state in HBM under an event tree:
                                       <= 256 nodes, links + flows <= 262 144,
-                                      identity overlays (ER-256), signalling type
-                                      "ideal" without big signalling              */
+                                      <= 4 096 generators, identity overlays
+                                      (ER-256); every signalling type            */
 
 /* signalling type (prisma_params_t.signaling_type, argument_parser.py:72 /
    sim.cc:142, 373-392): the payload of the --train small-signalling echo a node

@@ -305,6 +305,12 @@ struct Sim {
     const CAS int32_t* m_fsrc;
     const CAS int32_t* m_fdst;
     const CAS double* m_fmean;
+    const CAS uint32_t* m_esz;              // ... and the signalling arrays of the --train instances
+    const CAS uint32_t* m_etx;
+    const CAS uint32_t* m_abtx;
+    const CAS uint32_t* m_bpair;
+    const CAS uint32_t* m_fseq;
+    const CAS BigSig* m_bs;
     uint32_t* lrec;                         // link records [L][kLRec] (HBM)
 #if PRISMA_TIMING
     mutable uint64_t tsub[2], tlast;             // sub-phase cycles inside apply_decision
@@ -359,6 +365,15 @@ __device__ __forceinline__ int64_t t_acctx(const Sim& S, uint32_t u) { return S.
 __device__ __forceinline__ int32_t t_fsrc(const Sim& S, uint32_t f) { return S.mem ? S.m_fsrc[f] : S.T->fsrc[f]; }
 __device__ __forceinline__ int32_t t_fdst(const Sim& S, uint32_t f) { return S.mem ? S.m_fdst[f] : S.T->fdst[f]; }
 __device__ __forceinline__ double t_fmean(const Sim& S, uint32_t f) { return S.mem ? S.m_fmean[f] : S.T->fmean[f]; }
+__device__ __forceinline__ uint32_t t_esz(const Sim& S, uint32_t l) { return S.mem ? S.m_esz[l] : S.T->esz[l]; }
+__device__ __forceinline__ uint32_t t_etx(const Sim& S, uint32_t l) { return S.mem ? S.m_etx[l] : S.T->etx[l]; }
+__device__ __forceinline__ uint32_t t_abtx(const Sim& S, uint32_t u) { return S.mem ? S.m_abtx[u] : S.T->abtx[u]; }
+__device__ __forceinline__ uint32_t t_bpair(const Sim& S, uint32_t g) { return S.mem ? S.m_bpair[g] : S.T->bpair[g]; }
+__device__ __forceinline__ uint32_t t_fseq(const Sim& S, uint32_t f) { return S.mem ? S.m_fseq[f] : S.T->fseq[f]; }
+__device__ __forceinline__ uint32_t t_ngen(const Sim& S) { return S.mem ? S.m_bs->n_gen : S.T->n_bsig; }
+__device__ __forceinline__ uint32_t t_bs_nseg(const Sim& S) { return S.mem ? S.m_bs->nseg : S.T->bs_nseg; }
+__device__ __forceinline__ uint32_t t_bs_size(const Sim& S) { return S.mem ? S.m_bs->size : S.T->bs_size; }
+__device__ __forceinline__ int64_t t_bs_period(const Sim& S) { return S.mem ? S.m_bs->period : S.T->bs_period; }
 
 // A store to replica state that every lane may read back, by every lane (same address, same
 // value): no exec-mask juggling in LDS, and in HBM each lane's later read of the address is
@@ -432,9 +447,9 @@ __device__ __forceinline__ bool key_less(int64_t t, uint32_t s, int64_t bt, uint
 // know the big-signalling segment; the other instances never see either.
 __device__ __forceinline__ uint32_t ent_size(const Sim& S, uint32_t x, uint32_t l) {
     const LV& L = S.lv;
-    if (S.ctrl && !S.mem) {
-        if (ent_is_echo(x)) return S.T->esz[l];
-        if (ent_is_big(x)) return S.T->bs_size;
+    if (S.ctrl) {
+        if (ent_is_echo(x)) return t_esz(S, l);
+        if (ent_is_big(x)) return t_bs_size(S);
     }
     return ent_is_data(x) ? L.data_size() : (ent_is_echo(x) ? L.echo_size() : L.ping_size());
 }
@@ -641,10 +656,14 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
     const bool sw = l < (uint32_t)L.E();
     // register-resident engine: a switch link's tx time by entry class from the topology image
     // (--train instances: an echo's by link, sized by its sender)
-    int64_t tx = sw ? (S.mem ? (ent_is_data(x) ? L.sw_txd() : (ent_is_echo(x) ? L.sw_txe() : L.sw_txp()))
+    // (memory-resident: by entry type from the scenario constants; --train instances: echoes by
+    // link, big-signalling segments from the BigSig header)
+    int64_t tx = sw ? (S.mem ? ((S.ctrl && ent_is_echo(x)) ? (int64_t)t_etx(S, l)
+                                : ((S.ctrl && ent_is_big(x)) ? (int64_t)S.m_bs->tx_sw
+                                   : (ent_is_data(x) ? L.sw_txd() : (ent_is_echo(x) ? L.sw_txe() : L.sw_txp()))))
                              : (int64_t)((S.ctrl && ent_is_echo(x)) ? S.T->etx[l] : S.T->ctx[ent_cls(x)]))
-                    : ((S.ctrl && !S.mem && ent_is_big(x)) ? (int64_t)S.T->abtx[l - (uint32_t)L.E()]
-                                                           : t_acctx(S, l - (uint32_t)L.E()));
+                    : ((S.ctrl && ent_is_big(x)) ? (int64_t)t_abtx(S, l - (uint32_t)L.E())
+                                                 : t_acctx(S, l - (uint32_t)L.E()));
     int64_t prop = sw ? L.sw_prop() : 0;
     k.busy = 1;
     k.cp_t = lo32(H.now + tx);
@@ -1019,16 +1038,16 @@ __device__ __forceinline__ void flow_next(const Sim& S, RS& R, Hot& H, uint32_t 
 template <class RS>
 __device__ __forceinline__ void on_bsig(const Sim& S, RS& R, Hot& H, uint32_t f) {
     const uint32_t k = flow_draw(S, R, f);
-    const uint32_t G = S.T->n_bsig, E = (uint32_t)S.lv.E();
-    if (k > kUidMask) fail(H, PRISMA_EBIT_TIME);                    // 21-bit send index
+    const uint32_t G = t_ngen(S), E = (uint32_t)S.lv.E();
+    if (k > kGenSendMask) fail(H, PRISMA_EBIT_TIME);                // 17-bit send index (host-checked)
     uint32_t first = 0;
     for (uint32_t g = 0; g < G; ++g) {
-        if (k != 0 && !link_send(S, R, H, E + (S.T->bpair[g] & 255u), g_make(g, k))) CNT_ADD(S, ctrl_dropped, 1u);
+        if (k != 0 && !link_send(S, R, H, E + bp_src(t_bpair(S, g)), g_make(g, k))) CNT_ADD(S, ctrl_dropped, 1u);
         const uint32_t sq = H.seq++;
         if (g == 0) first = sq;
     }
     H.ev_launch += G - 1u;
-    flow_set(S, R, H, f, H.now + S.T->bs_period, first, k + 1u);
+    flow_set(S, R, H, f, H.now + t_bs_period(S), first, k + 1u);
 }
 
 template <class RS>
@@ -1037,6 +1056,7 @@ __device__ __forceinline__ void on_flow(const Sim& S, RS& R, Hot& H, uint32_t f)
     // flow block's are in flight together (one HBM round trip)
     uint32_t draw;
     if constexpr (RS::kMem) {
+        if (S.ctrl && f >= (uint32_t)S.lv.F()) { on_bsig(S, R, H, f); return; }
         const uint32_t acc = (uint32_t)S.lv.E() + (uint32_t)t_fsrc(S, f);
         const LinkV k = link_get(R, acc);
         draw = flow_draw(S, R, f);
@@ -1500,18 +1520,18 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         return 1;
     }
     wire_pop(S, R, H, l, k);
-    if (S.ctrl && !S.mem && ent_is_big(x)) {                        // (only with --signaling and --train)
-        const uint32_t bp = S.T->bpair[g_gen(x)];
-        const uint32_t src = bp & 255u, dst = (bp >> 8) & 255u;
+    if (S.ctrl && ent_is_big(x)) {                                  // (only with --signaling and --train)
+        const uint32_t bp = t_bpair(S, g_gen(x));
+        const uint32_t src = bp_src(bp), dst = bp_dst(bp);
         if (v == src) {                  // from the traffic node: IP-forwarded towards its destination
-            if (!link_send(S, R, H, (bp >> 16) & 255u, x)) CNT_ADD(S, ctrl_dropped, 1u);
+            if (!link_send(S, R, H, bp_link(bp), x)) CNT_ADD(S, ctrl_dropped, 1u);
             return 0;
         }
         if (tun && v != dst) { ctrl_forward(S, R, H, v, dst, x); return 0; }
         // BigSignalingPacketManager::receivePacket (big-signaling-packet-manager.cc:93-108):
         // at its destination, not its source -> Notify; obs [1000] (+ NN / segment index, sender)
         if (!fused && L.notify_dest()) {
-            const uint32_t n = g_n(x), ns = S.T->bs_nseg;
+            const uint32_t n = g_n(x), ns = t_bs_nseg(S);
             const uint32_t nn = ns <= 1u ? n : n / ns, seg = ns <= 1u ? 0u : n % ns;
             const uint32_t so = 0x10000u | (tun ? (uint32_t)S.T->ovi[src] : src);
             D.x = x; D.v = v; D.uid = 0u; D.flags = PEND_CTRL; D.last = 0u;

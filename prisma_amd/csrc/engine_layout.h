@@ -32,19 +32,27 @@ constexpr uint32_t K_PING = 0u, K_FLOW = 1u, K_COMPLETE = 2u, K_ARRIVE = 3u;
 //            bits 2-9 = its destination node (the data packet's last hop),
 //            bits 10-30 = the signalled data packet's uid mod 2^21
 //   big      big-signalling segment (--signaling, "NN"): T_PFWD with bit 31 set,
-//            bits 2-9 = its generator (TopoImage::bpair), bits 10-30 = the
-//            generator's send index (segment and NN index derive from it)
+//            bits 2-13 = its generator (bpair: up to 4096, one per flow between
+//            overlay neighbours -- 2 008 on ER-256), bits 14-30 = the generator's
+//            send index (segment and NN index derive from it; < 2^17 per episode,
+//            checked on the host)
 constexpr uint32_t T_RELAY = 0u, T_FRESH = 1u, T_PFWD = 2u, T_PBACK = 3u;
 constexpr uint32_t kEchoBit = 1u << 31;
 __host__ __device__ inline uint32_t ent_type(uint32_t x) { return x & 3u; }
 __host__ __device__ inline bool ent_is_data(uint32_t x) { return (x & 2u) == 0u; }
 __host__ __device__ inline bool ent_is_echo(uint32_t x) { return (x & (kEchoBit | 3u)) == (kEchoBit | T_PBACK); }
 __host__ __device__ inline bool ent_is_big(uint32_t x) { return (x & (kEchoBit | 3u)) == (kEchoBit | T_PFWD); }
+constexpr uint32_t kGenBits = 12u, kGenSendBits = 17u, kGenSendMask = (1u << kGenSendBits) - 1u;
 __host__ __device__ inline uint32_t g_make(uint32_t gen, uint32_t n) {
-    return T_PFWD | kEchoBit | (gen << 2) | ((n & ((1u << 21) - 1u)) << 10);
+    return T_PFWD | kEchoBit | (gen << 2) | ((n & kGenSendMask) << (2u + kGenBits));
 }
-__host__ __device__ inline uint32_t g_gen(uint32_t x) { return (x >> 2) & 255u; }
-__host__ __device__ inline uint32_t g_n(uint32_t x) { return (x >> 10) & ((1u << 21) - 1u); }
+__host__ __device__ inline uint32_t g_gen(uint32_t x) { return (x >> 2) & ((1u << kGenBits) - 1u); }
+__host__ __device__ inline uint32_t g_n(uint32_t x) { return (x >> (2u + kGenBits)) & kGenSendMask; }
+// big-signalling generator g: source | destination << 8 | first link << 16 (switch link ids
+// below 2^16: the memory-resident engine's ER-256 has 2 008)
+__host__ __device__ inline uint32_t bp_src(uint32_t bp) { return bp & 255u; }
+__host__ __device__ inline uint32_t bp_dst(uint32_t bp) { return (bp >> 8) & 255u; }
+__host__ __device__ inline uint32_t bp_link(uint32_t bp) { return bp >> 16; }
 __host__ __device__ inline uint32_t r_make(uint32_t dec, uint32_t src) {
     return T_RELAY | ((dec & ((1u << 22) - 1u)) << 2) | (src << 24);
 }
@@ -130,7 +138,7 @@ struct TopoImage {
                                  // + 30 B: one hop on identity overlays, uniform on tunnelled ones)
     uint32_t etx[256];           // ... and its transmission time (ns)
     uint32_t abtx[256];          // access link of node u: transmission time of a big-signalling segment
-    uint32_t bpair[256];         // big-signalling generator g: source | destination << 8 | first link << 16
+    uint32_t bpair[256];         // big-signalling generator g: source | destination << 8 | first link << 16 (bp_*)
     uint32_t fseq[512];          // start-event seq of flow slot f (data flows; slot F: generator 0)
     int64_t  bs_period;          // generator send period (ns)
     uint32_t n_bsig;             // generators (all in flow slot F)
@@ -183,12 +191,24 @@ struct Layout {
     uint32_t s_lkey, s_lkind;    // LDS offsets of the link leaf keys (time lo, seq) and kinds (bytes)
     // topology image offsets (memory-resident engine; variable-size arrays)
     uint32_t t_rowptr, t_ldst, t_lrev, t_acctx, t_fsrc, t_fdst, t_fmean;
+    // ... and its signalling arrays (the --train instances): echo size / tx time per switch
+    // link, big-segment tx time per access link, generators, start seqs, BigSig header
+    uint32_t t_esz, t_etx, t_abtx, t_bpair, t_fseq, t_bsig;
     // register-resident engine: the [N][N] action table is staged into LDS (after the state
     // image) only where that costs no replica per CU; otherwise it is read from HBM (L2)
     uint32_t table_in_lds;
     uint32_t lds_mlp_bytes;      // LDS of a DQN-buffer launch (its 256 B of activations included)
 };
 constexpr uint32_t kLVWords = 64u;           // Layout dwords held in the LV register
+
+// memory-resident engine: big-signalling constants (topology image at Layout::t_bsig)
+struct BigSig {
+    int64_t  period;             // generator send period (ns)
+    uint32_t n_gen;              // generators (one event slot: flow slot F)
+    uint32_t nseg;               // segments per NN copy
+    uint32_t size;               // segment size on the wire (542 B)
+    uint32_t tx_sw;              // its transmission time on a switch link (ns)
+};
 
 // memory-resident engine: one record of Layout::lrec_words (32 or 64) u32 words per
 // link, accessed lane j <-> word j (one coalesced load / masked store per access)

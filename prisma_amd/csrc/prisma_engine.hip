@@ -334,7 +334,9 @@ static int plan_overlay(const prisma_topology_t* T, OverlayPlan& OP) {
         if (len > 8) return set_err(PRISMA_ERR_CONFIG, "tunnel longer than 8 links (3-bit responder position)");
         OP.plen = len > OP.plen ? len : OP.plen;
         const int l0 = ident ? t : hop[(size_t)u * N + w];
-        OP.tinfo[t] = (uint32_t)l0 | ((uint32_t)w << 8) | ((uint32_t)u << 16) | ((uint32_t)len << 24);
+        // (identity overlays never read it back -- tunnel t is link t -- and their link ids may
+        // exceed the 8-bit field: ER-256)
+        OP.tinfo[t] = ((uint32_t)l0 & 255u) | ((uint32_t)w << 8) | ((uint32_t)u << 16) | ((uint32_t)len << 24);
         // forward path of the pings; a ping-back from every overlay node on it
         // (reverse of the arrival link, then routed to the origin); the --train
         // echo from the target likewise
@@ -415,6 +417,15 @@ static void compact_links(const prisma_topology_t* T, OverlayPlan& OP, prisma_to
     TC.link_rev = rev.data();
 }
 
+// Signalling tables of the --train instances (build_layout), for either engine's topology image
+struct Signal {
+    std::vector<uint32_t> esz, etx;              // per switch link: echo size (B), its tx time (ns)
+    std::vector<uint32_t> abtx;                  // per node: big segment's access-link tx time (ns)
+    std::vector<uint32_t> bpair;                 // per generator (bp_*)
+    std::vector<uint32_t> fseq;                  // [F + 1] start seqs of the flow slots
+    BigSig bs;
+};
+
 // Memory-resident engine (prisma_engine_mem.hip, identity overlays): topology as
 // variable-size arrays; state image = LDS part (header, counters, pending obs,
 // event-tree levels 1-2, link leaf keys) + HBM part (link records, flow leaf keys,
@@ -422,11 +433,13 @@ static void compact_links(const prisma_topology_t* T, OverlayPlan& OP, prisma_to
 // by build_layout.
 static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layout& L,
                       std::vector<unsigned char>& topo, const std::vector<int64_t>& acctx,
-                      const std::vector<int32_t>& ldst, uint32_t ring_total) {
+                      const std::vector<int32_t>& ldst, uint32_t ring_total, const Signal& SG) {
     const int N = T->n_nodes, E = T->n_links, F = T->n_flows, Lk = E + N;
     if (L.WCAP > (int)kMemMaxWire) return set_err(PRISMA_ERR_CONFIG, "more than 16 packets on a wire (memory-resident engine)");
     L.lrec_words = LR_WT + 3u * (uint32_t)L.WCAP <= 32u ? 32u : 64u;
-    const uint64_t n_leaf = (uint64_t)Lk + (uint64_t)F;
+    // event sources: links, flows, and the big-signalling generators' one slot (on_bsig)
+    const uint32_t FG = (uint32_t)F + (SG.bs.n_gen ? 1u : 0u);
+    const uint64_t n_leaf = (uint64_t)Lk + (uint64_t)FG;
     if (n_leaf > 64ull * 64ull * 64ull) return set_err(PRISMA_ERR_CONFIG, "more than 262 144 links + flows per replica");
     L.mem = 1;
     L.n_leaf = (uint32_t)n_leaf;
@@ -441,6 +454,12 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
     L.t_fsrc = take(4u * (uint64_t)F);
     L.t_fdst = take(4u * (uint64_t)F);
     L.t_fmean = take(8u * (uint64_t)F);
+    L.t_esz = take(4u * (uint64_t)E);
+    L.t_etx = take(4u * (uint64_t)E);
+    L.t_abtx = take(4u * (uint64_t)N);
+    L.t_bpair = take(4u * (uint64_t)(SG.bpair.size() ? SG.bpair.size() : 1u));
+    L.t_fseq = take(4u * (uint64_t)(F + 1));
+    L.t_bsig = take(sizeof(BigSig));
     L.topo_bytes = (uint32_t)o;
     topo.assign(o, 0);
     unsigned char* tb = topo.data();
@@ -453,6 +472,12 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
     double* fm = (double*)(tb + L.t_fmean);
     for (int f = 0; f < F; ++f)                      // poisson-application.cc:280-283
         fm[f] = (double)(P->packet_size * 8u) / (double)T->flow_rate_bps[f];
+    memcpy(tb + L.t_esz, SG.esz.data(), 4u * (size_t)E);
+    memcpy(tb + L.t_etx, SG.etx.data(), 4u * (size_t)E);
+    memcpy(tb + L.t_abtx, SG.abtx.data(), 4u * (size_t)N);
+    if (!SG.bpair.empty()) memcpy(tb + L.t_bpair, SG.bpair.data(), 4u * SG.bpair.size());
+    memcpy(tb + L.t_fseq, SG.fseq.data(), 4u * (size_t)(F + 1));
+    memcpy(tb + L.t_bsig, &SG.bs, sizeof(BigSig));
     o = 0;
     L.s_hdr = take(sizeof(Hdr));
     L.s_cnt = take(sizeof(prisma_counters_t));
@@ -465,7 +490,7 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
     L.s_lkind = take((uint64_t)Lk);
     L.lds_state_bytes = (uint32_t)o;
     L.g_lrec = take(4u * L.lrec_words * (uint64_t)Lk);
-    L.g_keys = take(16u * (uint64_t)F);
+    L.g_keys = take(16u * (uint64_t)FG);
     L.s_ring = take(4u * (uint64_t)ring_total);
     L.s_win = take(4u * (uint64_t)E * L.MA);
     L.s_pbd = take(4u * (uint64_t)E * L.PBK);
@@ -564,14 +589,19 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
             return set_err(PRISMA_ERR_CONFIG, "big signalling needs sync_step_s > 0 and big_signaling_bytes > 0");
         for (int f = 0; f < F; ++f) {
             const int u = T->flow_src[f], w = T->flow_dst[f];
-            for (int t = OP.ovrow[u]; t < OP.ovrow[u + 1]; ++t)
-                if ((int)ti_tgt(OP.tinfo[t]) == w) {
+            for (int t = OP.ovrow[u]; t < OP.ovrow[u + 1]; ++t) {
+                // (tinfo packs 8-bit link ids: on identity overlays tunnel t is switch link t,
+                // beyond 255 on the memory-resident engine's ER-256, so read the topology)
+                const int tgt = OP.tunnels ? (int)ti_tgt(OP.tinfo[t]) : T->link_dst[t];
+                if (tgt == w) {
+                    const uint32_t first = OP.tunnels ? ti_link(OP.tinfo[t]) : (uint32_t)t;
                     gen_of[f] = (int32_t)bpair.size();
-                    bpair.push_back((uint32_t)u | ((uint32_t)w << 8) | (ti_link(OP.tinfo[t]) << 16));
+                    bpair.push_back((uint32_t)u | ((uint32_t)w << 8) | (first << 16));
                     break;
                 }
+            }
         }
-        if (bpair.size() > 256u) return set_err(PRISMA_ERR_CONFIG, "more than 256 big-signalling generators");
+        if (bpair.size() > (1u << kGenBits)) return set_err(PRISMA_ERR_CONFIG, "more than 4096 big-signalling generators");
     }
     const int G = (int)bpair.size();
     // ScheduleNextTx's period in the reference's arithmetic (big-signaling-application.cc:247-250):
@@ -581,6 +611,9 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     // (the generators share one event slot: a period must outlast an access-link transmission)
     if (bsig && (bs_period < 1000 || bs_period >= ((int64_t)1 << 40)))
         return set_err(PRISMA_ERR_CONFIG, "big-signalling period out of range [1 us, 2^40 ns)");
+    // (a segment carries its generator's send index in 17 bits: engine_layout.h g_make)
+    if (bsig && sec_to_ns(P->sim_time_s) / bs_period + 2 > (int64_t)kGenSendMask)
+        return set_err(PRISMA_ERR_CONFIG, "more than 2^17 big-signalling sends per generator and episode");
     const uint32_t bs_size = 512u + 30u;
 
     memset(&L, 0, sizeof(L));
@@ -705,23 +738,51 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
                              4u * (uint32_t)OP.T * L.MA +
                              4u * (uint32_t)(OP.tunnels ? OP.n_resp : OP.T) * L.PBK + 1024u + 16u * (1u + L.W) +
                              (uint32_t)(N * N);
-    const bool reg_fits = N <= 255 && Lk <= 256 && E <= 256 && FG <= 512 && OP.T <= 256 && fs <= 8 && ls <= 4 &&
+    const bool reg_fits = N <= 255 && Lk <= 256 && E <= 256 && FG <= 512 && OP.T <= 256 && G <= 256 && fs <= 8 && ls <= 4 &&
                           tot <= 65535u && reg_lds + 256u <= 160u * 1024u;
     uint32_t engine = P->engine == PRISMA_ENGINE_AUTO ? (reg_fits ? PRISMA_ENGINE_REGISTER : PRISMA_ENGINE_MEMORY)
                                                       : P->engine;
     if (engine == PRISMA_ENGINE_REGISTER && !reg_fits)
         return set_err(PRISMA_ERR_CONFIG, "topology exceeds the register-resident engine (255 nodes, 256 links / "
-                                          "tunnels, 512 flows, 160 KiB LDS); use PRISMA_ENGINE_MEMORY");
+                                          "tunnels / generators, 512 flows, 160 KiB LDS); use PRISMA_ENGINE_MEMORY");
     if (engine == PRISMA_ENGINE_MEMORY && OP.tunnels)
         return set_err(PRISMA_ERR_CONFIG, "the memory-resident engine runs identity overlays only");
-    if (engine == PRISMA_ENGINE_MEMORY && (P->signaling_type != PRISMA_SIGNALING_IDEAL || G))
-        return set_err(PRISMA_ERR_CONFIG, "the memory-resident engine runs signalling type \"ideal\" without big "
-                                          "signalling");
+    // signalling arrays (both engines): echo size / tx time per switch link (echoes leave node u
+    // on its own links), big-segment tx time per access link, start seqs of the flow slots (the
+    // ping timers, then the apps in install order: each generator right after its flow; slot F
+    // holds generator 0's)
+    Signal SG;
+    SG.esz.resize(E);
+    SG.etx.resize(E);
+    for (int u = 0; u < N; ++u)
+        for (int l = T->row_ptr[u]; l < T->row_ptr[u + 1]; ++l) {
+            SG.esz[l] = (OP.tunnels ? epay[OP.ovnode[0]] : epay[u]) + 30u;
+            SG.etx[l] = (uint32_t)sec_to_ns((double)SG.esz[l] * 8 / (double)P->link_bps);
+        }
+    SG.abtx.resize(N);
+    for (int u = 0; u < N; ++u)
+        SG.abtx[u] = (uint32_t)sec_to_ns((double)bs_size * 8 / (double)((uint64_t)1000000 * P->link_bps * (uint64_t)pdeg[u]));
+    SG.bpair = bpair;
+    SG.fseq.assign(F + 1, 0u);
+    {
+        uint32_t q = (uint32_t)OP.NO;
+        for (int f = 0; f < F; ++f) {
+            SG.fseq[f] = q++;
+            if (gen_of[f] == 0) SG.fseq[F] = q;      // generator 0 opens the group's slot
+            if (gen_of[f] >= 0) q++;
+        }
+        if (!G) SG.fseq[F] = q;
+    }
+    SG.bs.period = bs_period;
+    SG.bs.n_gen = (uint32_t)G;
+    SG.bs.nseg = bsig ? P->big_signaling_bytes / 512u : 0u;
+    SG.bs.size = bs_size;
+    SG.bs.tx_sw = (uint32_t)sec_to_ns((double)bs_size * 8 / (double)P->link_bps);
     uint32_t o = 0;
     auto take = [&](uint32_t bytes) { uint32_t r = o; o = align16(o + bytes); return r; };
     L.table_bytes = (uint32_t)(N * N);
     if (engine == PRISMA_ENGINE_MEMORY)
-        return layout_mem(T, P, L, topo, acctx, ldst, tot);
+        return layout_mem(T, P, L, topo, acctx, ldst, tot, SG);
     // topology image
     L.topo_bytes = (uint32_t)sizeof(TopoImage) + (OP.tunnels ? 4u * (uint32_t)(N * N) : 0u);
     topo.assign(L.topo_bytes, 0);
@@ -752,27 +813,16 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
         TI.ctx[c] = (uint32_t)(data ? L.sw_txd : (echo ? L.sw_txe : (big ? sec_to_ns((double)bs_size * 8 / (double)P->link_bps)
                                                                          : L.sw_txp)));
     }
-    for (int u = 0; u < N; ++u)                      // echoes leave node u on its own links
-        for (int l = T->row_ptr[u]; l < T->row_ptr[u + 1]; ++l) {
-            const uint32_t sz = (OP.tunnels ? epay[OP.ovnode[0]] : epay[u]) + 30u;
-            TI.esz[l] = sz;
-            TI.etx[l] = (uint32_t)sec_to_ns((double)sz * 8 / (double)P->link_bps);
-        }
-    for (int u = 0; u < N; ++u)
-        TI.abtx[u] = (uint32_t)sec_to_ns((double)bs_size * 8 / (double)((uint64_t)1000000 * P->link_bps * (uint64_t)pdeg[u]));
+    memcpy(TI.esz, SG.esz.data(), 4u * E);
+    memcpy(TI.etx, SG.etx.data(), 4u * E);
+    memcpy(TI.abtx, SG.abtx.data(), 4u * N);
     for (int g = 0; g < G; ++g) TI.bpair[g] = bpair[g];
-    {                                                // start events: ping timers, then apps in install order
-        uint32_t q = (uint32_t)OP.NO;
-        for (int f = 0; f < F; ++f) {
-            TI.fseq[f] = q++;
-            if (gen_of[f] == 0) TI.fseq[F] = q;      // generator 0 opens the group's slot
-            if (gen_of[f] >= 0) q++;
-        }
-    }
-    TI.bs_period = bs_period;
-    TI.n_bsig = (uint32_t)G;
-    TI.bs_nseg = bsig ? P->big_signaling_bytes / 512u : 0u;
-    TI.bs_size = bs_size;
+    for (int f = 0; f < F; ++f) TI.fseq[f] = SG.fseq[f];
+    if (G) TI.fseq[F] = SG.fseq[F];
+    TI.bs_period = SG.bs.period;
+    TI.n_bsig = SG.bs.n_gen;
+    TI.bs_nseg = SG.bs.nseg;
+    TI.bs_size = SG.bs.size;
     if (OP.tunnels) memcpy(topo.data() + sizeof(TopoImage), OP.route.data(), 4u * (size_t)N * N);
 
     // state image: LDS part (staged into LDS) then register part (staged into VGPRs)

@@ -348,6 +348,12 @@ __device__ __forceinline__ void mem_bind(Sim& S, MemSt& R, const KParams& P, con
     S.m_fsrc = (const CAS int32_t*)(tb + LC.t_fsrc);
     S.m_fdst = (const CAS int32_t*)(tb + LC.t_fdst);
     S.m_fmean = (const CAS double*)(tb + LC.t_fmean);
+    S.m_esz = (const CAS uint32_t*)(tb + LC.t_esz);
+    S.m_etx = (const CAS uint32_t*)(tb + LC.t_etx);
+    S.m_abtx = (const CAS uint32_t*)(tb + LC.t_abtx);
+    S.m_bpair = (const CAS uint32_t*)(tb + LC.t_bpair);
+    S.m_fseq = (const CAS uint32_t*)(tb + LC.t_fseq);
+    S.m_bs = (const CAS BigSig*)(tb + LC.t_bsig);
     R.lrec = S.lrec;
     R.fkeys = (uint4*)(img + LC.g_keys);
     R.lkey = (uint2*)(lds + LC.s_lkey);
@@ -384,16 +390,22 @@ __device__ __forceinline__ void init_replica(Sim& S, MemSt& R, Hot& H, uint32_t 
         for (uint32_t l = 0; l < NL; ++l) R.lrec[l * R.RW + j] = v;
     }
     // flow leaves (link leaves are in LDS, zeroed: no event); lane j writes the leaves
-    // 64b + j that its block reductions read back
+    // 64b + j that its block reductions read back.  Start seqs: the NO ping timers, then the
+    // apps in install order (fseq: with big signalling each generator right after its flow);
+    // leaf F is the generators' slot (on_bsig), started at AppStartTime (sim.cc:244, 645)
+    const uint32_t nbs = S.m_bs->n_gen;
     for (uint32_t i = j; i < R.n_leaf; i += kWave) {
         if (i < NL) continue;
         const uint32_t f = i - NL;
-        uint32_t c[4] = { f, 0u, episode, 0u };
-        philox4x32_10(c, L.seed_lo(), S.gid);
-        uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
-        double U = (double)u53 * (1.0 / 9007199254740992.0);
-        const int64_t t = sec_to_ns(0.0001 + U);                 // sim.cc:610-630
-        R.fkeys[f] = make_uint4(lo32(t), hi32(t), (uint32_t)L.NO() + f, 0u);   // after the NO ping timers
+        int64_t t = sec_to_ns(0.0001);
+        if (f < (uint32_t)L.F()) {
+            uint32_t c[4] = { f, 0u, episode, 0u };
+            philox4x32_10(c, L.seed_lo(), S.gid);
+            uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
+            double U = (double)u53 * (1.0 / 9007199254740992.0);
+            t = sec_to_ns(0.0001 + U);                                // sim.cc:610-630
+        }
+        R.fkeys[f] = make_uint4(lo32(t), hi32(t), S.m_fseq[f], 0u);
     }
     __syncthreads();
     for (uint32_t b = 0; b < R.n1; ++b) lds_put_key(S, &R.lv1[b], block_min(S, R, b, 0));
@@ -402,7 +414,7 @@ __device__ __forceinline__ void init_replica(Sim& S, MemSt& R, Hot& H, uint32_t 
     H.now = 0;
     H.ping_t = L.ping_period();
     H.ping_seq = 0;
-    H.seq = (uint32_t)L.NO() + (uint32_t)L.F();
+    H.seq = (uint32_t)L.NO() + (uint32_t)L.F() + nbs;
     H.uid = 0; H.ping_rounds = 0; H.pend = 0; H.over = 0; H.error = 0; H.stop = 0;
     H.dec = dec; H.hops_launch = hl; H.ev_launch = el;
     H.episode = episode;

@@ -216,3 +216,104 @@ def test_er256_full_size_properties(oracle_mod):
     assert np.all(cnt["ov_injected"] >= cnt["ov_arrived"] + cnt["ov_lost"])
     assert np.all(cnt["bytes_data"] == 540 * cnt["ov_injected"])
     assert len(np.unique(cnt["now_ns"])) > R // 2
+
+
+# ---- signalling on the memory engine (sim.cc:373-392, 634-647) ------------------------
+def _sig(topo, **kw):
+    base = dict(sim_time_s=4.0, ping_as_obs=1, train=1, signaling_type="NN", big_signaling=1, replica_base=3,
+                big_signaling_bytes=35328, engine=MEM)
+    base.update(kw)
+    return engine_params(topo, **base)
+
+
+@pytest.mark.parametrize("name,tm,lf,kw", [
+    ("abilene", 0, 1.0, dict()),
+    ("abilene", 1, 2.0, dict(sync_step_s=0.1, seed=7)),                 # 10x the segments, drops
+    ("abilene", 0, 1.0, dict(ping_as_obs=0, big_signaling_bytes=4096, sync_step_s=0.05)),
+    ("abilene", 2, 1.5, dict(signaling_type="target", big_signaling=0)),
+    ("geant", 0, 1.0, dict(sync_step_s=0.5)),                           # per-node echo sizes
+])
+def test_mem_signaling_table_parity(oracle_mod, name, tm, lf, kw):
+    """Echo payloads by signalling type and the big-signalling generators on the memory engine
+    (forced), bit-exact against the oracle: the register engine's signalling cases."""
+    topo = Topology.example(name, tm, lf)
+    cnt = run_both(oracle_mod, topo, _sig(topo, **kw), 4, 2500, sp_next_hop_table(topo))
+    assert int(cnt["bytes_signaling"].min()) > 0
+
+
+def test_mem_signaling_equals_register_engine():
+    """Big signalling: both engines produce byte-identical logs and counters (GEANT, 32 replicas)."""
+    topo = Topology.example("geant", 0, 1.5)
+    table = torch.from_numpy(sp_next_hop_table(topo)).cuda()
+    out = []
+    for kind in (PRISMA_ENGINE_REGISTER, MEM):
+        eng = PrismaEngine(topo, _sig(topo, sim_time_s=10.0, sync_step_s=0.25, engine=kind), 32)
+        assert eng.engine_kind == kind
+        eng.reset(0)
+        eng.run(table, 4000)
+        torch.cuda.synchronize()
+        out.append((eng.log_tensor().cpu().numpy(), eng.counters()))
+        eng.close()
+    assert int(out[1][1]["ctrl_dropped"].sum()) >= 0 and int(out[1][1]["bytes_signaling"].min()) > 0
+    assert np.array_equal(out[0][0], out[1][0])
+    assert out[0][1].tobytes() == out[1][1].tobytes()
+
+
+def test_mem_signaling_external_notify_parity(oracle_mod):
+    """notify_dest + train + big signalling on the memory engine: echo and NN-segment
+    notifications reach the caller with the obs fields of include/prisma.h."""
+    topo = Topology.example("abilene", 0, 1.5)
+    params = _sig(topo, sim_time_s=2.0, notify_dest=1, sync_step_s=0.2)
+    R = 3
+    eng = PrismaEngine(topo, params, R)
+    assert eng.engine_kind == MEM
+    eng.reset(0)
+    orcs = [oracle_mod.OracleSim(topo, params, replica=params["replica_base"] + r) for r in range(R)]
+    ref_obs = [o.step(-1) for o in orcs]
+    obs, mask, node = eng.step(None)
+    rng = np.random.default_rng(19)
+    n_big = n_echo = 0
+    for s in range(1500):
+        g, m, nd = obs.cpu().numpy(), mask.cpu().numpy(), node.cpu().numpy()
+        acts = np.zeros(R, dtype=np.int32)
+        for r in range(R):
+            assert (ref_obs[r] is None) == (m[r] == 0), (s, r)
+            if ref_obs[r] is None:
+                continue
+            assert np.array_equal(ref_obs[r], g[r]), (s, r, g[r], ref_obs[r])
+            assert nd[r] == orcs[r].pending_node()
+            if g[r][0] == 1000:
+                n_big += int(g[r][3] >> 16)
+                n_echo += 1 - int(g[r][3] >> 16)
+            acts[r] = rng.integers(0, topo.degrees[nd[r]])
+        ref_obs = [orcs[r].step(int(acts[r])) if ref_obs[r] is not None else None for r in range(R)]
+        obs, mask, node = eng.step(torch.from_numpy(acts).cuda())
+    torch.cuda.synchronize()
+    assert n_big > 0 and n_echo > 0
+    cnt = eng.counters()
+    log = eng.log_tensor().cpu().numpy()
+    for r in range(R):
+        ref = orcs[r].records()
+        assert eng.records(r, 0, len(ref), log_host=log).tobytes() == ref.tobytes()
+        assert_counters_equal(cnt[r], orcs[r].counters(), r)
+    eng.close()
+
+
+def test_er256_big_signaling_parity(oracle_mod):
+    """Config 5's graph with --train, "NN" echoes and big signalling: 2 006 generators (one per
+    flow between neighbours), beyond the register engine's 256, all in one event slot."""
+    topo, table = er256()
+    params = _sig(topo, sim_time_s=60.0, sync_step_s=0.5, seed=11, replica_base=77, engine=0)
+    cnt = run_both(oracle_mod, topo, params, 2, 6000, table, launches=2)
+    assert int(cnt["bytes_signaling"].min()) > 0
+
+
+def test_er256_big_signaling_dqn_buffer_parity(oracle_mod):
+    """... and with the in-kernel DQN-buffer agent deciding (the memory engine's MLP + CTRL
+    instance)."""
+    from prisma_amd.policies import StackedQNet
+    topo, _ = er256()
+    w = StackedQNet(topo, "buffer", seed=8).pack()
+    params = _sig(topo, sim_time_s=60.0, ping_as_obs=1, sync_step_s=0.25, seed=5, replica_base=9, engine=0)
+    run_both(oracle_mod, topo, params, 2, 3000, w, launches=2, mlp=True,
+             net_cpu=StackedQNet(topo, "buffer", seed=8, device="cpu"))

@@ -145,15 +145,22 @@ def test_parse_arguments_signaling_flags():
 
 
 def test_plan_rejects_unsupported_signaling():
-    """prisma_plan (no device): the memory-resident engine and tunnelled overlays with
-    per-node echo sizes refuse instead of running a different model."""
-    from prisma_amd.engine import PRISMA_ENGINE_MEMORY, PrismaError, plan
+    """prisma_plan (no device): both engines plan every signalling type on identity overlays
+    (ER-256's 2 006 generators only fit the memory-resident engine); tunnelled overlays with
+    per-node echo sizes and send indices beyond the 17-bit segment field refuse instead of
+    running a different model."""
+    from prisma_amd.engine import PRISMA_ENGINE_MEMORY, PRISMA_ENGINE_REGISTER, PrismaError, plan
     topo = Topology.example("abilene")
     assert plan(topo, big_params(topo))["flow_slots"] >= 1
-    with pytest.raises(PrismaError, match="memory-resident"):
-        plan(topo, big_params(topo, engine=PRISMA_ENGINE_MEMORY))
-    with pytest.raises(PrismaError, match="memory-resident"):
-        plan(topo, engine_params(topo, train=1, signaling_type="target", engine=PRISMA_ENGINE_MEMORY))
+    assert plan(topo, big_params(topo, engine=PRISMA_ENGINE_MEMORY))["engine"] == PRISMA_ENGINE_MEMORY
+    assert plan(topo, engine_params(topo, train=1, signaling_type="target",
+                                    engine=PRISMA_ENGINE_MEMORY))["engine"] == PRISMA_ENGINE_MEMORY
+    er = Topology.example("er256")
+    assert plan(er, big_params(er))["engine"] == PRISMA_ENGINE_MEMORY
+    with pytest.raises(PrismaError, match="register-resident"):
+        plan(er, big_params(er, engine=PRISMA_ENGINE_REGISTER))
+    with pytest.raises(PrismaError, match="2\\^17"):
+        plan(topo, big_params(topo, sync_step_s=0.001))
     aog = Topology.example("abilene_on_geant")                    # overlay degrees 2..4
     with pytest.raises(PrismaError, match="equal overlay"):
         plan(aog, big_params(aog))
