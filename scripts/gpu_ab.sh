@@ -9,6 +9,13 @@ WARM=${4:-5}
 mkdir -p gpurun_out
 CONFIGS=("headline|" "geant_dqn|--topology geant --policy dqn_buffer --ping-as-obs 0 --replicas 2048"
          "aog_dqn|--topology abilene_on_geant --policy dqn_buffer")
+# AB_CONFIGS="name ..." picks a subset; er256_dqn / er256_sp are config 5 (warmed past the transient)
+CONFIGS+=("er256_dqn|--topology er256 --policy dqn_buffer --warmup 13" "er256_sp|--topology er256 --policy sp --warmup 13")
+if [ -n "$AB_CONFIGS" ]; then
+  SEL=()
+  for c in "${CONFIGS[@]}"; do for n in $AB_CONFIGS; do [ "${c%%|*}" = "$n" ] && SEL+=("$c"); done; done
+  CONFIGS=("${SEL[@]}")
+fi
 for i in 1 2; do
   for c in "${CONFIGS[@]}"; do
     name=${c%%|*}; args=${c#*|}
