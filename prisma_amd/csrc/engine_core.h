@@ -453,9 +453,8 @@ __device__ __forceinline__ uint32_t ent_size(const Sim& S, uint32_t x, uint32_t 
     }
     return ent_is_data(x) ? L.data_size() : (ent_is_echo(x) ? L.echo_size() : L.ping_size());
 }
-// whole seconds of a (non-negative) time: unsigned division by a constant is shorter
-// scalar code than the signed one (A/B: +1 % at the headline)
-#define TSEC(t) ((uint64_t)(t) / 1000000000u)
+// whole seconds of a (non-negative) time, on the vector unit (numerics.h div_1e9)
+#define TSEC(t) div_1e9((uint64_t)(t))
 // class of entry x (type | echo bit << 2): index of TopoImage::ctx
 __device__ __forceinline__ uint32_t ent_cls(uint32_t x) { return (x & 3u) | ((x >> 29) & 4u); }
 // FIFO ring of link l: uniform capacities on identity overlays, per-link (sized by the

@@ -113,10 +113,31 @@ __host__ __device__ inline int64_t sec_to_ns(double s) { return (int64_t)(s * 1e
 // ns-3 Time::GetSeconds()
 __host__ __device__ inline double ns_to_sec(int64_t t) { return (double)t / 1e9; }
 
+// t / 1000 and t / 10^9 for 0 <= t < 2^42 ns (sim_time_s <= 4095, checked on the host) on the
+// vector unit: floor(t * c) with c the double nearest 10^-3 (10^-9) is exact there -- both
+// doubles lie above the true reciprocals, so a multiple of the divisor never lands below its
+// quotient, and any other t sits at least 1/divisor above an integer, far beyond the product's
+// rounding error (< 2^-20 here).  The scalar unit's 64-bit division by a constant is ~18
+// instructions, and the scalar unit is the headline kernel's busiest resource.
+__host__ __device__ inline uint64_t div_1e3(uint64_t t) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return (uint64_t)(uint32_t)__builtin_floor((double)t * 0.001);
+#else
+    return t / 1000u;
+#endif
+}
+__host__ __device__ inline uint64_t div_1e9(uint64_t t) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return (uint64_t)(uint32_t)__builtin_floor((double)t * 1e-9);
+#else
+    return t / 1000000000u;
+#endif
+}
+
 // microseconds of std::to_string(GetSeconds()) (%f, ties-to-even on the
 // exact binary value) as Python reads them back (packet-manager.cc:127-128).
 __host__ __device__ inline uint64_t py_micros(int64_t t) {
-    uint64_t u = (uint64_t)t / 1000u;                   // t >= 0
+    uint64_t u = div_1e3((uint64_t)t);                  // t >= 0
     int64_t r = t - (int64_t)u * 1000;
     if (r != 500) return r < 500 ? u : u + 1;
     double x = ns_to_sec(t);
