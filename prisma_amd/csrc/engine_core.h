@@ -765,9 +765,11 @@ __device__ __forceinline__ void on_complete(const Sim& S, RS& R, Hot& H, uint32_
 // ---- observation (data-packet-manager.cc:171-206)
 // send time in seconds of ping round k as the ping-back manager stores it:
 // (double)GetMilliSeconds() * 0.001 (ping-back-packet-manager.cc:98-116)
+// floor((k + 1) period / 10^6) on the vector unit: the product is exact (< 2^42 ns), and the
+// reciprocal of 10^6 rounded up keeps a multiple of 10^6 on its quotient (numerics.h div_1e3)
 __device__ __forceinline__ double ping_send_s(const LV& L, int64_t k) {
-    uint64_t ms = (uint64_t)((k + 1) * L.ping_period()) / 1000000u;
-    return (double)ms * 0.001;
+    const double ms = __builtin_floor((double)(k + 1) * (double)L.ping_period() * 0x1.0c6f7a0b5ed8ep-20);
+    return ms * 0.001;
 }
 
 __device__ __forceinline__ double ld_d(uint32_t lo, uint32_t hi) {
@@ -1013,12 +1015,14 @@ __device__ __forceinline__ void on_ping_round(const Sim& S, RS& R, Hot& H) {   /
 template <class RS>
 __device__ __forceinline__ void flow_next(const Sim& S, RS& R, Hot& H, uint32_t f, uint32_t draw) {
     uint32_t c[4] = { f, draw, H.episode, 1u };                   // poisson-application.cc:265-295
-    // table-policy instances: the key is opaque here, so its ten round keys are derived per
-    // call (two s_add a round) instead of hoisted out of the event loop into 18 SGPRs (A/B
-    // +0.6 % at the headline); the MLP instances keep them hoisted (opaque: config 4 -2.5 %)
+    // The table-policy instances run the rounds on the vector unit (the values pass through
+    // VGPRs, so the compiler cannot keep them scalar) and take back the two words they use:
+    // ~80 scalar instructions per flow event moved off the headline's busiest unit.  The MLP
+    // instances keep the scalar rounds with their keys hoisted out of the event loop.
     uint32_t k0 = S.lv.seed_lo(), k1 = S.gid;
-    if (!S.mlp_inst) asm volatile("" : "+s"(k0), "+s"(k1));
+    if (!S.mlp_inst) asm volatile("" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(k0), "+v"(k1));
     philox4x32_10(c, k0, k1);
+    if (!S.mlp_inst) { c[0] = __builtin_amdgcn_readfirstlane(c[0]); c[1] = __builtin_amdgcn_readfirstlane(c[1]); }
     uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
     double U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
     double delay = -t_fmean(S, f) * det_log(U);

@@ -19,7 +19,8 @@ fi
 for i in 1 2; do
   for c in "${CONFIGS[@]}"; do
     name=${c%%|*}; args=${c#*|}
-    for lib in $VARS new; do
+    # AB_NO_NEW=1: variants only (the working tree's sources no longer match the in-tree library)
+    for lib in $VARS $([ -n "$AB_NO_NEW" ] || echo new); do
       if [ $lib = new ]; then unset PRISMA_LIB; else export PRISMA_LIB=$PWD/prisma_amd/_ablate/libprisma_amd_$lib.so; fi
       out=gpurun_out/ab_${TAG}_${name}_${lib}_$i.json
       timeout -k 10 200 python bench.py --cpu-baseline 0 --steps $STEPS --warmup $WARM $args > $out || exit 1
