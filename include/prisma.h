@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PRISMA_ABI_VERSION 7
+#define PRISMA_ABI_VERSION 8
 
 /* status codes */
 #define PRISMA_OK              0
@@ -86,6 +86,17 @@ extern "C" {
 #define PRISMA_SIGNALING_IDEAL  0
 #define PRISMA_SIGNALING_NN     1
 #define PRISMA_SIGNALING_TARGET 2
+
+/* random streams (prisma_params_t.rng_mode) */
+#define PRISMA_RNG_PHILOX 0        /* counter-based Philox4x32-10 per (seed, replica, flow,
+                                      draw, episode): replicas and episodes independent [default] */
+#define PRISMA_RNG_NS3    1        /* ns-3's RngStream MRG32k3a (rng-stream.cc): one stream per
+                                      RandomVariable object in creation order -- a Uniform per flow
+                                      for its start offset (sim.cc:610-620), then per packet the
+                                      Uniform of SendPacket (poisson-application.cc:311) and the
+                                      Exponential of ScheduleNextTx (:281); simSeed = seed +
+                                      replica id as seed and run (sim.cc:253-254), the same streams
+                                      every episode (run_ns3.py restarts ns-3 with the same seed) */
 
 /* per-decision status (prisma_record_t.status) */
 #define PRISMA_ST_PENDING      0   /* waiting for an action (prisma_step)  */
@@ -183,6 +194,12 @@ typedef struct prisma_params {
                                    application.cc:224-309)                 */
     float    sync_step_s;       /* syncStep: seconds per NN copy   [1.0]   */
     uint32_t big_signaling_bytes; /* bigSignalingSize: NN bytes   [35328]  */
+    /* ---- ABI 8 ---- */
+    uint32_t rng_mode;          /* PRISMA_RNG_*                    [0]     */
+    uint32_t rng_stream_offset; /* PRISMA_RNG_NS3: streams ns-3 itself
+                                   creates before sim.cc's flow loop (ARP,
+                                   ICMPv6, global routing of every node;
+                                   version-dependent, so a parameter)      */
 } prisma_params_t;
 
 /*

@@ -39,7 +39,7 @@ class OrConfig(C.Structure):
         ("ov_row_ptr", C.POINTER(C.c_int32)), ("tun_dst", C.POINTER(C.c_int32)),
         ("tun_link", C.POINTER(C.c_int32)), ("next_link", C.POINTER(C.c_int32)),
         ("signaling_type", C.c_uint32), ("big_signaling", C.c_uint32), ("sync_step_s", C.c_float),
-        ("big_signaling_bytes", C.c_uint32),
+        ("big_signaling_bytes", C.c_uint32), ("rng_mode", C.c_uint32), ("rng_stream_offset", C.c_uint32),
     ]
 
 
@@ -94,6 +94,9 @@ def lib():
         L.or_seconds_to_ns.argtypes = [C.c_double]
         L.or_py_micros.restype = C.c_uint64
         L.or_py_micros.argtypes = [C.c_int64]
+        L.or_mrg_pow2.argtypes = [C.c_int, C.POINTER(C.c_uint64)]
+        L.or_mrg_first_u01.restype = C.c_double
+        L.or_mrg_first_u01.argtypes = [C.c_uint32, C.c_uint64, C.c_uint64]
         _lib = L
     return _lib
 
@@ -172,6 +175,8 @@ class OracleSim:
         cfg.big_signaling = int(params.get("big_signaling", 0))
         cfg.sync_step_s = float(params.get("sync_step_s", 1.0))
         cfg.big_signaling_bytes = int(params.get("big_signaling_bytes", 512))
+        cfg.rng_mode = int(params.get("rng_mode", 0))
+        cfg.rng_stream_offset = int(params.get("rng_stream_offset", 0))
         self._cfg = cfg
         self.W = topo.obs_width
         self.rec_dtype = record_dtype(self.W)

@@ -167,8 +167,93 @@ typedef struct {              /* temp_obs entry (forwarder.py:153-159) */
     int64_t dec; int64_t t_ns; int active;
 } temp_t;
 
+/* ---- ns-3 random streams (rng_mode 1): RngStream, rng-stream.cc --------------------------
+ * MRG32k3a (L'Ecuyer 1999) with the package's stream construction: a RandomVariableStream
+ * created k-th in a run draws from RngStream(seed, k, run): all six state words = seed, then
+ * AdvanceNthBy(k, 127) and AdvanceNthBy(run, 76), i.e. for every set bit i of k the state is
+ * multiplied by A^(2^(127+i)) (and likewise for the run with 76).  RandU01 is the package's
+ * double arithmetic. */
+static const uint64_t or_m1 = 4294967087ull, or_m2 = 4294944443ull;
+
+static void mrg_matmul(const uint64_t* X, const uint64_t* Y, uint64_t* Z) {   /* [18] each */
+    uint64_t t[18];
+    for (int c = 0; c < 2; ++c) {
+        const uint64_t m = c ? or_m2 : or_m1;
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) {
+                uint64_t acc = 0;
+                for (int k = 0; k < 3; ++k) acc = (acc + X[9 * c + 3 * i + k] * Y[9 * c + 3 * k + j] % m) % m;
+                t[9 * c + 3 * i + j] = acc;
+            }
+    }
+    memcpy(Z, t, sizeof(t));
+}
+
+void or_mrg_pow2(int e, uint64_t out[18]) {
+    uint64_t A[18] = { 0, 1, 0, 0, 0, 1, or_m1 - 810728u, 1403580u, 0,
+                       0, 1, 0, 0, 0, 1, or_m2 - 1370589u, 0, 527612u };
+    for (int i = 0; i < e; ++i) mrg_matmul(A, A, A);
+    memcpy(out, A, sizeof(A));
+}
+
+static void mrg_matvec(const uint64_t* M, uint64_t* v) {
+    uint64_t r[6];
+    for (int c = 0; c < 2; ++c) {
+        const uint64_t m = c ? or_m2 : or_m1;
+        for (int i = 0; i < 3; ++i) {
+            uint64_t acc = 0;
+            for (int k = 0; k < 3; ++k) acc = (acc + M[9 * c + 3 * i + k] * v[3 * c + k] % m) % m;
+            r[3 * c + i] = acc;
+        }
+    }
+    memcpy(v, r, sizeof(r));
+}
+
+static double mrg_rand_u01(uint64_t* st) {                      /* RngStream::RandU01 */
+    double p1 = 1403580.0 * (double)st[1] - 810728.0 * (double)st[0];
+    int64_t k = (int64_t)(p1 / 4294967087.0);
+    p1 -= (double)k * 4294967087.0;
+    if (p1 < 0.0) p1 += 4294967087.0;
+    st[0] = st[1]; st[1] = st[2]; st[2] = (uint64_t)p1;
+    double p2 = 527612.0 * (double)st[5] - 1370589.0 * (double)st[3];
+    k = (int64_t)(p2 / 4294944443.0);
+    p2 -= (double)k * 4294944443.0;
+    if (p2 < 0.0) p2 += 4294944443.0;
+    st[3] = st[4]; st[4] = st[5]; st[5] = (uint64_t)p2;
+    return (p1 > p2) ? (p1 - p2) * 2.328306549295727688e-10 : (p1 - p2 + 4294967087.0) * 2.328306549295727688e-10;
+}
+
+/* A^(2^(127+i)) for i < 64 and A^(2^(76+i)) for i < 64, built once */
+static uint64_t g_mrg_p127[64][18], g_mrg_p76[64][18];
+static int g_mrg_ready = 0;
+static void mrg_tables(void) {
+    if (g_mrg_ready) return;
+    uint64_t A[18];
+    or_mrg_pow2(76, A);
+    for (int i = 0; i < 51 + 64; ++i) {         /* A = A^(2^(76+i)); 76 + 51 = 127 */
+        if (i < 64) memcpy(g_mrg_p76[i], A, sizeof(A));
+        if (i >= 51) memcpy(g_mrg_p127[i - 51], A, sizeof(A));
+        mrg_matmul(A, A, A);
+    }
+    g_mrg_ready = 1;
+}
+
+static void mrg_stream_state(uint32_t seed, uint64_t stream, uint64_t run, uint64_t st[6]) {
+    mrg_tables();
+    for (int i = 0; i < 6; ++i) st[i] = seed;
+    for (int i = 0; i < 64; ++i) if ((stream >> i) & 1u) mrg_matvec(g_mrg_p127[i], st);   /* AdvanceNthBy(stream, 127) */
+    for (int i = 0; i < 64; ++i) if ((run >> i) & 1u) mrg_matvec(g_mrg_p76[i], st);       /* AdvanceNthBy(run, 76) */
+}
+
+double or_mrg_first_u01(uint32_t seed, uint64_t stream, uint64_t run) {
+    uint64_t st[6];
+    mrg_stream_state(seed, stream, run, st);
+    return mrg_rand_u01(st);
+}
+
 struct or_sim {
     or_config_t c;
+    uint64_t rv_next;           /* rng_mode 1: stream of the next RandomVariable object created */
     int N, E, F, W;
     int64_t t_end, ping_period, now;
     uint64_t seq;
@@ -639,13 +724,23 @@ static void bsig_index(const or_sim_t* s, uint32_t n, uint32_t* nn, uint32_t* se
     *nn = n / s->bs_nseg; *seg = n % s->bs_nseg;
 }
 
+/* rng_mode 1: simSeed of this replica (sim.cc:253-254 set it as seed and run) */
+static uint32_t ns3_sim_seed(const or_sim_t* s) { return (uint32_t)(s->c.seed + s->c.replica); }
+
 static void flow_schedule_next(or_sim_t* s, int f) {                /* poisson-application.cc:265-295 */
-    uint32_t key[2] = { (uint32_t)s->c.seed, s->c.replica };
-    uint32_t ctr[4] = { (uint32_t)f, (uint32_t)s->flow_draws[f], s->c.episode, 1u };
-    uint32_t x[4];
-    or_philox4x32_10(ctr, key, x);
-    uint64_t u53 = ((uint64_t)(x[0] >> 5) << 26) | (uint64_t)(x[1] >> 6);
-    double U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
+    double U;
+    if (s->c.rng_mode == 1) {
+        /* a new ExponentialRandomVariable per packet (:281-284): its stream's first value */
+        const uint32_t sd = ns3_sim_seed(s);
+        U = or_mrg_first_u01(sd, s->rv_next++, sd);
+    } else {
+        uint32_t key[2] = { (uint32_t)s->c.seed, s->c.replica };
+        uint32_t ctr[4] = { (uint32_t)f, (uint32_t)s->flow_draws[f], s->c.episode, 1u };
+        uint32_t x[4];
+        or_philox4x32_10(ctr, key, x);
+        uint64_t u53 = ((uint64_t)(x[0] >> 5) << 26) | (uint64_t)(x[1] >> 6);
+        U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
+    }
     double delay = -s->flow_mean[f] * or_det_log(U);
     s->flow_draws[f]++;
     schedule(s, s->now + or_seconds_to_ns(delay), EV_SEND, f, -1);
@@ -660,6 +755,7 @@ static void flow_send_packet(or_sim_t* s, int f) {                  /* poisson-a
     k->last_hop = 1000;
     k->start_time = (uint64_t)get_seconds(s->now);                    /* :310 */
     k->valable = 1;                                                   /* overlay pair: p = 1.0 */
+    if (s->c.rng_mode == 1) s->rv_next++;       /* the UniformRandomVariable of :311-314 (its value: the tag above) */
     k->uid = s->next_uid++;
     k->ttl = 255;                                                     /* SetIpTtl(255) :330 */
     k->size = s->c.packet_size + 8 + 20 + 2;
@@ -919,12 +1015,20 @@ or_sim_t* or_create(const or_config_t* cfg) {
        flow (src, dst) order (sim.cc:599-631) */
     for (int i = 0; i < cfg->n_overlay; ++i) schedule(s, s->ping_period, EV_PING, cfg->overlay_nodes[i], -1);
     uint32_t key[2] = { (uint32_t)cfg->seed, cfg->replica };
+    s->rv_next = cfg->rng_stream_offset;
     for (int f = 0; f < s->F; ++f) {
-        uint32_t ctr[4] = { (uint32_t)f, 0u, cfg->episode, 0u };
-        uint32_t x[4];
-        or_philox4x32_10(ctr, key, x);
-        uint64_t u53 = ((uint64_t)(x[0] >> 5) << 26) | (uint64_t)(x[1] >> 6);
-        double U = (double)u53 * (1.0 / 9007199254740992.0);
+        double U;
+        if (cfg->rng_mode == 1) {
+            /* the UniformRandomVariable of flow f's start offset, created in the flow loop */
+            const uint32_t sd = ns3_sim_seed(s);
+            U = or_mrg_first_u01(sd, s->rv_next++, sd);
+        } else {
+            uint32_t ctr[4] = { (uint32_t)f, 0u, cfg->episode, 0u };
+            uint32_t x[4];
+            or_philox4x32_10(ctr, key, x);
+            uint64_t u53 = ((uint64_t)(x[0] >> 5) << 26) | (uint64_t)(x[1] >> 6);
+            U = (double)u53 * (1.0 / 9007199254740992.0);
+        }
         schedule(s, or_seconds_to_ns(0.0001 + U), EV_START, f, -1);
         if (g_of_flow[f] >= 0) schedule(s, or_seconds_to_ns(0.0001), EV_BSTART, g_of_flow[f], -1);   /* AppStartTime */
     }

@@ -64,6 +64,11 @@ typedef struct or_config {
     uint32_t big_signaling;     /* --signaling: NN-weight generators (with NN and train) */
     float    sync_step_s;       /* syncStep                                  */
     uint32_t big_signaling_bytes; /* bigSignalingSize                        */
+    /* random streams: 0 Philox (the engine's default), 1 ns-3's RngStream MRG32k3a with one
+       stream per RandomVariable object in creation order (simSeed = seed + replica as seed and
+       run; streams from rng_stream_offset on: the objects ns-3 itself creates first) */
+    uint32_t rng_mode;
+    uint32_t rng_stream_offset;
 } or_config_t;
 
 typedef struct or_sim or_sim_t;
@@ -115,6 +120,11 @@ int32_t or_last_info(const or_sim_t* s, char* buf, int32_t cap);
 
 /* Exposed building blocks for known-answer tests. */
 void     or_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]);
+/* ns-3 RngStream (rng-stream.cc, L'Ecuyer et al. 2002): A1^(2^e) mod m1 and A2^(2^e) mod m2
+   (out[0..8], out[9..17], row-major), and the first RandU01 of stream `stream`, substream `run`
+   of package seed `seed` */
+void     or_mrg_pow2(int e, uint64_t out[18]);
+double   or_mrg_first_u01(uint32_t seed, uint64_t stream, uint64_t run);
 double   or_det_log(double x);
 int64_t  or_seconds_to_ns(double s);
 uint64_t or_py_micros(int64_t t_ns);

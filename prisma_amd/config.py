@@ -21,6 +21,7 @@ DEFAULTS = dict(
     loss_penalty_type="fixed", signalingSim=0, sync_step=1.0, bigSignalingSize=512,
 )
 SIGNALING_TYPES = {"ideal": 0, "NN": 1, "target": 2}      # include/prisma.h PRISMA_SIGNALING_*
+RNG_MODES = {"philox": 0, "ns3": 1}                           # include/prisma.h PRISMA_RNG_*
 
 AGENT_TYPES = ["dqn_buffer", "dqn_routing", "dqn_buffer_fp", "dqn_buffer_lite", "dqn_buffer_lighter",
                "dqn_buffer_lighter_2", "dqn_buffer_lighter_3", "dqn_buffer_ff",
@@ -74,7 +75,8 @@ def engine_params(topo: Topology, *, sim_time_s: float = 60.0, seed: int = 100, 
                   auto_reset: int = 0, log_capacity: int = 8192, replica_base: int = 0,
                   loss_penalty: Optional[float] = None, train: int = 0, notify_dest: int = 0,
                   engine: int = 0, signaling_type="ideal", big_signaling: int = 0, sync_step_s: float = 1.0,
-                  big_signaling_bytes: int = DEFAULTS["bigSignalingSize"]) -> dict:
+                  big_signaling_bytes: int = DEFAULTS["bigSignalingSize"], rng: str = "philox",
+                  rng_stream_offset: int = 0) -> dict:
     """prisma_params_t as a dict (shared by the engine binding and the oracle).
 
     train=1 is the reference's --train: every data notification at a non-source
@@ -86,7 +88,11 @@ def engine_params(topo: Topology, *, sim_time_s: float = 60.0, seed: int = 100, 
     big_signaling_bytes every sync_step_s between overlay neighbours (sim.cc:634-647; run_ns3.py
     passes signalingSim, sync_step and bigSignalingSize, whose argument_parser.py:74 default, 512 B = one
     segment per NN, is the default here too; sim.cc's own default is 35328).  The simulator switches --signaling off
-    for the sp / opt agents and for "ideal" (sim.cc:374-376): the caller's part, as in run_ns3.py."""
+    for the sp / opt agents and for "ideal" (sim.cc:374-376): the caller's part, as in run_ns3.py.
+    rng: "philox" (counter-based streams per replica, flow, draw and episode) or "ns3" (ns-3's
+    MRG32k3a RngStream streams, one per RandomVariable object in the reference's creation order,
+    simSeed = seed + replica id; rng_stream_offset = the streams ns-3 creates before sim.cc's flow
+    loop, include/prisma.h PRISMA_RNG_NS3)."""
     if log_capacity < 1024 or log_capacity > (1 << 22) or log_capacity & (log_capacity - 1):
         raise ValueError("log_capacity must be a power of two in [1024, 2^22]")
     lp = _loss_penalty(max_buffer, packet_size, link_cap, topo.n_overlay) if loss_penalty is None else loss_penalty
@@ -101,4 +107,5 @@ def engine_params(topo: Topology, *, sim_time_s: float = 60.0, seed: int = 100, 
         replica_base=int(replica_base), log_capacity=int(log_capacity), notify_dest=int(notify_dest),
         train=int(train), engine=int(engine), signaling_type=st, big_signaling=int(big_signaling),
         sync_step_s=float(sync_step_s), big_signaling_bytes=int(big_signaling_bytes),
+        rng_mode=RNG_MODES[rng] if isinstance(rng, str) else int(rng), rng_stream_offset=int(rng_stream_offset),
     )

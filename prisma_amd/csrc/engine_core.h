@@ -18,6 +18,7 @@
 #include "../../include/prisma.h"
 #include "engine_layout.h"
 #include "numerics.h"
+#include "mrg32k3a.h"
 
 using namespace prisma;
 
@@ -75,6 +76,7 @@ struct KParams {
     int32_t mode;                // 0 reset, 1 external step, 2 table run, 3 auto-reset, 4 MLP run
     unsigned char* spare;        // [R][state_bytes] next-episode images (register engine with
                                  // auto_reset), or null
+    const uint32_t* rng;         // ns-3 stream mode: the rng table (engine_layout.h kMrgPowers), or null
 };
 
 // ---------------------------------------------------------------------------
@@ -266,6 +268,7 @@ struct LV {
     __device__ __forceinline__ uint32_t rec_bytes() const { return (uint32_t)u(offsetof(Layout, rec_bytes) / 4); }
     __device__ __forceinline__ double loss_penalty() const { return __longlong_as_double(mk64(u(offsetof(Layout, loss_penalty) / 4), u(offsetof(Layout, loss_penalty) / 4 + 1))); }
     __device__ __forceinline__ float loss_penalty_f() const { return __uint_as_float(u(offsetof(Layout, loss_penalty_f) / 4)); }
+    __device__ __forceinline__ uint32_t rng_mode() const { return (uint32_t)u(offsetof(Layout, rng_mode) / 4); }
 };
 
 
@@ -1012,8 +1015,56 @@ __device__ __forceinline__ void on_ping_round(const Sim& S, RS& R, Hot& H) {   /
     flow_min_refresh(S, R, H);
 }
 
+// ns-3 stream mode (PRISMA_RNG_NS3): the uniform of the ExponentialRandomVariable that
+// ScheduleNextTx creates for every packet (poisson-application.cc:281-284) -- the first value
+// of a new stream.  A packet's SendPacket creates a UniformRandomVariable first (:311-314; its
+// value only sets the tag's overlay flag, 1 for every flow here), so draws after the first skip
+// one stream.  State: the next stream's initial state and the jump J, in LDS (kRngBytes).
+__device__ __forceinline__ double ns3_exp_u01(const Sim& S, uint32_t draw) {
+    uint32_t* g = (uint32_t*)(S.base + S.lv.lds_state_bytes() - kRngBytes);
+    uint32_t st[6], J[18];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) st[i] = u_ld32(g + i);
+#pragma unroll
+    for (int i = 0; i < 18; ++i) J[i] = u_ld32(g + 8 + i);
+    if (draw != 0) mrg_apply(J, st);                              // SendPacket's uniform stream
+    uint32_t e[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) e[i] = st[i];
+    const double U = mrg_u01(e);
+    mrg_apply(J, st);
+#pragma unroll
+    for (int i = 0; i < 6; ++i) st_rep(S, g + i, st[i]);
+    return U;
+}
+
+// ns-3 stream mode at an episode start: flow f's start offset comes from the
+// UniformRandomVariable the flow loop creates for it (sim.cc:610-620), the f-th stream from
+// rng_stream_offset on -- state J^f T, from the table's powers of J -- and the LDS image gets
+// the run's first stream (the one after the flows') and J.  rep: the replica's table entry.
+__device__ __forceinline__ double ns3_start_u01(const uint32_t* rng, const uint32_t* rep, uint32_t f) {
+    uint32_t st[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) st[i] = rep[i];
+    for (uint32_t b = 0; b < kMrgPowers; ++b)
+        if ((f >> b) & 1u) mrg_apply(rng + 18u * b, st);
+    return mrg_u01(st);
+}
+__device__ __forceinline__ void ns3_init_lds(const Sim& S, const uint32_t* rng, const uint32_t* rep) {
+    uint32_t* g = (uint32_t*)(S.base + S.lv.lds_state_bytes() - kRngBytes);
+    if (S.lane < 6) g[S.lane] = rep[6 + S.lane];
+    else if (S.lane >= 8 && S.lane < 26) g[S.lane] = rng[S.lane - 8];
+}
+
 template <class RS>
 __device__ __forceinline__ void flow_next(const Sim& S, RS& R, Hot& H, uint32_t f, uint32_t draw) {
+    // (only the CTRL instances carry the ns-3 streams: the host picks them for rng_mode, so the
+    // Philox instances' event loop keeps its registers)
+    if (S.ctrl && S.lv.rng_mode()) {
+        const double delay = -t_fmean(S, f) * det_log(ns3_exp_u01(S, draw));
+        flow_set(S, R, H, f, H.now + sec_to_ns(delay), H.seq++, draw + 1);
+        return;
+    }
     uint32_t c[4] = { f, draw, H.episode, 1u };                   // poisson-application.cc:265-295
     // The table-policy instances run the rounds on the vector unit (the values pass through
     // VGPRs, so the compiler cannot keep them scalar) and take back the two words they use:
@@ -1601,7 +1652,9 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
 // ---------------------------------------------------------------------------
 // keep_totals: carry the header's hops_total / events_total over (auto-reset)
 template <int FS, int LS>
-__device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t episode, bool keep_totals) {
+// rng / r: the ns-3 stream table and the replica's local index (null: Philox streams)
+__device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, uint32_t episode, bool keep_totals,
+                                             const uint32_t* rng, uint32_t r) {
     const LV& L = S.lv;
     const int lane = S.lane;
     uint32_t dec = H.dec, hl = H.hops_launch, el = H.ev_launch;
@@ -1610,6 +1663,11 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
     __syncthreads();
     uint4* st4 = (uint4*)S.base;
     for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes() / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
+    const uint32_t* rep = rng ? rng + 18u * kMrgPowers + kMrgRepWords * r : nullptr;
+    if (rng) {
+        __syncthreads();
+        ns3_init_lds(S, rng, rep);
+    }
     // big-signalling generators: flow slot F (on_bsig), each generator started right after its
     // flow (sim.cc:599-647: the start events in install order, fseq)
     const bool bsig = S.ctrl && !S.mem;
@@ -1620,10 +1678,15 @@ __device__ __forceinline__ void init_replica(Sim& S, Regs<FS, LS>& R, Hot& H, ui
         int64_t t = INT64_MAX;
         uint32_t s = 0xffffffffu;
         if (f < (uint32_t)L.F()) {
-            uint32_t c[4] = { f, 0u, episode, 0u };
-            philox4x32_10(c, L.seed_lo(), S.gid);
-            uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
-            double U = (double)u53 * (1.0 / 9007199254740992.0);
+            double U;
+            if (rng) {
+                U = ns3_start_u01(rng, rep, f);
+            } else {
+                uint32_t c[4] = { f, 0u, episode, 0u };
+                philox4x32_10(c, L.seed_lo(), S.gid);
+                uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
+                U = (double)u53 * (1.0 / 9007199254740992.0);
+            }
             t = sec_to_ns(0.0001 + U);                              // sim.cc:610-630
             s = bsig ? S.T->fseq[f] : (uint32_t)L.NO() + f;    // after the NO ping timers
         } else if (nbs && f == (uint32_t)L.F()) {

@@ -178,7 +178,8 @@ struct Layout {
     uint32_t log_cap, rec_bytes;
     double   loss_penalty;
     float    loss_penalty_f;
-    uint32_t pad_lv;
+    uint32_t rng_mode;           // PRISMA_RNG_*; ns-3 streams keep their state in the last kRngBytes
+                                 // of the LDS image (engine_core.h ns3_exp_u01)
     // ---- dwords 64..: not in the LV register (read through the scalar cache) ----
     // memory-resident engine (mem = 1, prisma_engine_mem.hip): the LDS image holds
     // the header, counters, pending obs and the upper levels of the event tree;
@@ -200,6 +201,13 @@ struct Layout {
     uint32_t lds_mlp_bytes;      // LDS of a DQN-buffer launch (its 256 B of activations included)
 };
 constexpr uint32_t kLVWords = 64u;           // Layout dwords held in the LV register
+
+// ns-3 random streams (PRISMA_RNG_NS3, mrg32k3a.h): the replica's LDS image ends with the
+// initial state of the next stream to be created (words 0-5) and the one-stream jump J
+// (words 8-25); the engine's rng table (KParams::rng) holds J^(2^b), b < kMrgPowers, then
+// per replica the state of stream rng_stream_offset (its flows' start streams follow) and of
+// the first stream created while the simulation runs
+constexpr uint32_t kRngBytes = 112u, kMrgPowers = 18u, kMrgRepWords = 12u;
 
 // memory-resident engine: big-signalling constants (topology image at Layout::t_bsig)
 struct BigSig {

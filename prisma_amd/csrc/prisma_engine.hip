@@ -85,7 +85,7 @@ __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     }
     if (build) {
         Regs<FS, LS> R;
-        init_replica(S, R, H, episode, keep);
+        init_replica(S, R, H, episode, keep, P.rng, (uint32_t)r);
         hot_store(S, R, H);
         __syncthreads();
         publish_counters(S, P, r, lane);
@@ -98,7 +98,7 @@ __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
             Hot H2;
             memset(&H2, 0, sizeof(H2));
             Regs<FS, LS> R2;
-            init_replica(S, R2, H2, episode + 1u, false);   // log position and totals: patched at restart
+            init_replica(S, R2, H2, episode + 1u, false, P.rng, (uint32_t)r);   // log position and totals: patched at restart
             hot_store(S, R2, H2);
             __syncthreads();
             image_store(lds, LC, sp, lane, R2);
@@ -207,6 +207,7 @@ struct prisma_env {
     const void* k_reset = nullptr;
     float* d_mlp_rp = nullptr;           // interleaved DQN-buffer layers 2-4 (prisma_run, mode 4)
     unsigned char* d_spare = nullptr;    // next-episode images (register engine with auto_reset)
+    uint32_t* d_rng = nullptr;           // ns-3 stream table (PRISMA_RNG_NS3, engine_layout.h kMrgPowers)
     bool reset_done = false;
 };
 
@@ -488,6 +489,7 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
     L.s_lv2 = take(16u * L.n2);
     L.s_lkey = take(8u * (uint64_t)Lk);
     L.s_lkind = take((uint64_t)Lk);
+    if (L.rng_mode) take(kRngBytes);                // ns-3 streams: the last kRngBytes (engine_core.h)
     L.lds_state_bytes = (uint32_t)o;
     L.g_lrec = take(4u * L.lrec_words * (uint64_t)Lk);
     L.g_keys = take(16u * (uint64_t)FG);
@@ -563,6 +565,9 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
         return set_err(PRISMA_ERR_CONFIG, "sim_time_s must be in (0, 4095] (12-bit packet start second)");
     if (P->log_capacity < 1024 || P->log_capacity > (1u << 22) || (P->log_capacity & (P->log_capacity - 1)))
         return set_err(PRISMA_ERR_CONFIG, "log_capacity must be a power of two >= 1024");
+    if (P->rng_mode > PRISMA_RNG_NS3) return set_err(PRISMA_ERR_CONFIG, "rng_mode must be PRISMA_RNG_PHILOX or _NS3");
+    if (P->rng_mode == PRISMA_RNG_NS3 && (uint64_t)F >= (1ull << kMrgPowers))
+        return set_err(PRISMA_ERR_CONFIG, "ns-3 streams: more than 2^18 flows");
     if (P->signaling_type > PRISMA_SIGNALING_TARGET)
         return set_err(PRISMA_ERR_CONFIG, "signaling_type must be PRISMA_SIGNALING_IDEAL, _NN or _TARGET");
     // signalling (sim.cc:373-392): the echo payload of overlay node u by its overlay degree;
@@ -626,6 +631,7 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.ping_size = 8u + 30u;
     L.echo_size = 0u + 30u;                         // signalling type "ideal": 0-B payload (sim.cc:371-391)
     L.train = P->train ? 1u : 0u;
+    L.rng_mode = P->rng_mode;
     // link constants (sim.cc:398-433): switch links share rate, delay and queue
     L.sw_txd = sec_to_ns((double)L.data_size * 8 / (double)P->link_bps);
     L.sw_txp = sec_to_ns((double)L.ping_size * 8 / (double)P->link_bps);
@@ -842,6 +848,7 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     if (!OP.tunnels) L.s_ring = take(4u * tot);
     L.s_win = take(4u * (uint32_t)OP.T * L.MA);
     L.s_pbd = take(4u * (uint32_t)(OP.tunnels ? OP.n_resp : OP.T) * L.PBK);
+    if (L.rng_mode) take(kRngBytes);                // ns-3 streams: the last kRngBytes (engine_core.h)
     L.lds_state_bytes = o;
     if (OP.tunnels) L.s_ring = take(4u * tot);      // HBM part of the image
     L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 16u * 64u * (uint32_t)ls));
@@ -896,6 +903,44 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
         prisma_destroy(e);
         return set_err(PRISMA_ERR_NOMEM, "hipMalloc failed");
     }
+    if (L.rng_mode == PRISMA_RNG_NS3) {
+        // ns-3 streams (mrg32k3a.h): J^(2^b), then per replica the states of stream
+        // rng_stream_offset (its first flow's start) and of the run's first stream -- from the
+        // package seed simSeed in all six words, advanced by simSeed substreams (SetRun)
+        const uint64_t seed0 = params->seed + params->replica_base;
+        if (seed0 < 1 || seed0 + (uint64_t)n_replicas > kMrgM2) {
+            prisma_destroy(e);
+            return set_err(PRISMA_ERR_CONFIG, "ns-3 streams: seed + replica id must lie in [1, 4294944443)");
+        }
+        std::vector<uint32_t> tab(18u * kMrgPowers + (size_t)kMrgRepWords * n_replicas);
+        const MrgMat J = mrg_pow2(127);
+        MrgMat Jb = J;
+        for (uint32_t b = 0; b < kMrgPowers; ++b) {
+            memcpy(&tab[18u * b], Jb.a, sizeof(Jb.a));
+            Jb = mrg_mul(Jb, Jb);
+        }
+        const MrgMat JX = mrg_pow(J, params->rng_stream_offset);
+        const MrgMat JXF = mrg_pow(J, (uint64_t)params->rng_stream_offset + (uint64_t)topo->n_flows);
+        MrgMat sub[32];                                  // A^(2^(76+i)): AdvanceNthBy(run, 76)
+        sub[0] = mrg_pow2(76);
+        for (int i = 1; i < 32; ++i) sub[i] = mrg_mul(sub[i - 1], sub[i - 1]);
+        for (int32_t r = 0; r < n_replicas; ++r) {
+            const uint32_t sd = (uint32_t)(seed0 + (uint64_t)r);
+            uint32_t s0[6] = { sd, sd, sd, sd, sd, sd };
+            for (int i = 0; i < 32; ++i)
+                if ((sd >> i) & 1u) mrg_apply(sub[i].a, s0);
+            uint32_t* rep = &tab[18u * kMrgPowers + (size_t)kMrgRepWords * r];
+            memcpy(rep, s0, sizeof(s0));
+            mrg_apply(JX.a, rep);
+            memcpy(rep + 6, s0, sizeof(s0));
+            mrg_apply(JXF.a, rep + 6);
+        }
+        if (!HIP_OK(hipMalloc((void**)&e->d_rng, 4u * tab.size())) ||
+            !HIP_OK(hipMemcpy(e->d_rng, tab.data(), 4u * tab.size(), hipMemcpyHostToDevice))) {
+            prisma_destroy(e);
+            return set_err(PRISMA_ERR_NOMEM, "ns-3 stream table");
+        }
+    }
     // fused runs with auto_reset continue into the next episode from a prebuilt image
     // (engine_core.h spare_restart): one more state image per replica
     if (L.auto_reset && !L.mem && !HIP_OK(hipMalloc(&e->d_spare, sb))) {
@@ -910,13 +955,14 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
         return set_err(PRISMA_ERR_DEVICE, "device initialisation failed");
     }
     if (L.mem) {
-        const bool ctrl = L.train || L.notify_dest;
+        const bool ctrl = L.train || L.notify_dest || L.rng_mode;   // (ns-3 streams: CTRL instances, flow_next)
         e->k_step = prisma_mem_kernel(0, ctrl);
         e->k_reset = prisma_mem_kernel(1, ctrl);
         e->k_step_mlp = prisma_mem_kernel(2, ctrl);
     } else {
-        // the --train echo and notify_dest paths are compiled only into the instances that need them
-        const bool ctrl = L.train || L.notify_dest;
+        // the --train echo and notify_dest paths (and the ns-3 streams) are compiled only into the
+        // instances that need them
+        const bool ctrl = L.train || L.notify_dest || L.rng_mode;
         auto pick = ctrl ? pick_step_ctrl : prisma_pick_step_lite;
         e->k_step = pick(L.FS, L.LS, false, L.tunnels != 0u);
         e->k_reset = pick_reset(L.FS, L.LS);
@@ -939,6 +985,7 @@ static KParams base_params(prisma_env_t* e) {
     P.cnt_out = e->d_cnt;
     P.R = e->R;
     P.spare = e->d_spare;
+    P.rng = e->d_rng;
     return P;
 }
 
@@ -1117,5 +1164,6 @@ extern "C" void prisma_destroy(prisma_env_t* e) {
     if (e->d_lay) (void)hipFree(e->d_lay);
     if (e->d_mlp_rp) (void)hipFree(e->d_mlp_rp);
     if (e->d_spare) (void)hipFree(e->d_spare);
+    if (e->d_rng) (void)hipFree(e->d_rng);
     delete e;
 }

@@ -373,7 +373,8 @@ __device__ __forceinline__ void mem_bind(Sim& S, MemSt& R, const KParams& P, con
 // episode start (sim.cc:610-630, data-packet-manager.cc:118-121): LDS header,
 // counters and obs zeroed; link records cleared (ping: round 0 pending from its
 // send time on); link keys infinite; flow keys at their start offsets; tree built.
-__device__ __forceinline__ void init_replica(Sim& S, MemSt& R, Hot& H, uint32_t episode, bool keep_totals) {
+__device__ __forceinline__ void init_replica(Sim& S, MemSt& R, Hot& H, uint32_t episode, bool keep_totals,
+                                             const uint32_t* rng, uint32_t r) {
     const LV& L = S.lv;
     const int lane = S.lane;
     uint32_t dec = H.dec, hl = H.hops_launch, el = H.ev_launch;
@@ -382,6 +383,11 @@ __device__ __forceinline__ void init_replica(Sim& S, MemSt& R, Hot& H, uint32_t 
     __syncthreads();
     uint4* st4 = (uint4*)S.base;
     for (uint32_t i = (uint32_t)lane; i < L.lds_state_bytes() / 16u; i += kWave) st4[i] = make_uint4(0, 0, 0, 0);
+    const uint32_t* rep = rng ? rng + 18u * kMrgPowers + kMrgRepWords * r : nullptr;   // (engine_core.h)
+    if (rng) {
+        __syncthreads();
+        ns3_init_lds(S, rng, rep);
+    }
     const uint64_t od = (uint64_t)__double_as_longlong(ping_send_s(L, 0));
     const uint32_t NL = R.L;
     const uint32_t j = (uint32_t)lane;
@@ -399,10 +405,15 @@ __device__ __forceinline__ void init_replica(Sim& S, MemSt& R, Hot& H, uint32_t 
         const uint32_t f = i - NL;
         int64_t t = sec_to_ns(0.0001);
         if (f < (uint32_t)L.F()) {
-            uint32_t c[4] = { f, 0u, episode, 0u };
-            philox4x32_10(c, L.seed_lo(), S.gid);
-            uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
-            double U = (double)u53 * (1.0 / 9007199254740992.0);
+            double U;
+            if (rng) {
+                U = ns3_start_u01(rng, rep, f);
+            } else {
+                uint32_t c[4] = { f, 0u, episode, 0u };
+                philox4x32_10(c, L.seed_lo(), S.gid);
+                uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
+                U = (double)u53 * (1.0 / 9007199254740992.0);
+            }
             t = sec_to_ns(0.0001 + U);                                // sim.cc:610-630
         }
         R.fkeys[f] = make_uint4(lo32(t), hi32(t), S.m_fseq[f], 0u);
@@ -461,7 +472,7 @@ __global__ void __launch_bounds__(64) prisma_mem_reset_kernel(KParams P) {
     Sim S;
     MemSt R;
     mem_bind(S, R, P, lv, lds, r, lane);
-    init_replica(S, R, H, episode, keep);
+    init_replica(S, R, H, episode, keep, P.rng, (uint32_t)r);
     hot_store(S, R, H);
     __syncthreads();
     publish_counters(S, P, r, lane);

@@ -18,7 +18,7 @@ from .topology import Topology
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprisma_amd.so")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 PRISMA_POLICY_TABLE = 1
 PRISMA_POLICY_DQN_BUFFER = 2
 PRISMA_ENGINE_AUTO, PRISMA_ENGINE_REGISTER, PRISMA_ENGINE_MEMORY = 0, 1, 2
@@ -51,11 +51,13 @@ class _Params(C.Structure):
         ("log_capacity", C.c_uint32), ("notify_dest", C.c_uint32), ("train", C.c_uint32),
         ("engine", C.c_uint32), ("signaling_type", C.c_uint32), ("big_signaling", C.c_uint32),
         ("sync_step_s", C.c_float), ("big_signaling_bytes", C.c_uint32),
+        ("rng_mode", C.c_uint32), ("rng_stream_offset", C.c_uint32),
     ]
 
 
 # the defaults of config.engine_params (argument_parser.py:72-74, 86; bigSignalingSize 512)
-_PARAM_DEFAULTS = dict(engine=0, signaling_type=0, big_signaling=0, sync_step_s=1.0, big_signaling_bytes=512)
+_PARAM_DEFAULTS = dict(engine=0, signaling_type=0, big_signaling=0, sync_step_s=1.0, big_signaling_bytes=512,
+                       rng_mode=0, rng_stream_offset=0)
 
 
 class _LogView(C.Structure):
@@ -217,7 +219,7 @@ class PrismaEngine:
         # notify_dest paths are compiled in (step_kernel.h)
         pl = plan(topo, params)
         self.engine_kind = pl["engine"]
-        ctrl = "true" if (params.get("train") or params.get("notify_dest")) else "false"
+        ctrl = "true" if (params.get("train") or params.get("notify_dest") or params.get("rng_mode")) else "false"
         if self.engine_kind == PRISMA_ENGINE_MEMORY:
             self.kernel_name = f"prisma_mem_step_kernel<false, {ctrl}>"
             self.kernel_name_mlp = f"prisma_mem_step_kernel<true, {ctrl}>"

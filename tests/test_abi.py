@@ -32,7 +32,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = engine.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.prisma_abi_version() == engine.ABI_VERSION == 7
+    assert lib.prisma_abi_version() == engine.ABI_VERSION == 8
     out = subprocess.run(["nm", "-D", "--defined-only", engine.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (prisma_\w+)", out))
     assert set(declared_functions()) <= exported
