@@ -15,7 +15,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "prisma_amd", "csrc")
 
 ENGINE_SOURCES = ["prisma_engine.hip", "prisma_engine_lite.hip", "prisma_engine_mem.hip"]
-ENGINE_HEADERS = ["engine_core.h", "engine_layout.h", "numerics.h", "step_kernel.h"]
+ENGINE_HEADERS = ["engine_core.h", "engine_layout.h", "numerics.h", "step_kernel.h", "mrg32k3a.h"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC", "-std=c++17",
                # the per-replica counters are bumped by lane 0 only: the atomic optimizer's
                # wave-aggregation rewrite (mbcnt, bcnt, exec juggling per add) is pure overhead

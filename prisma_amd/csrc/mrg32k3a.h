@@ -21,8 +21,6 @@ constexpr uint64_t kMrgM1 = 4294967087ull, kMrgM2 = 4294944443ull;
 // one 3x3 matrix per component, row-major: [0..8] mod m1, [9..17] mod m2
 struct MrgMat { uint32_t a[18]; };
 
-__host__ __device__ inline uint32_t mrg_mod(uint64_t x, uint64_t m) { return (uint32_t)(x % m); }
-
 // s <- M s (both components)
 __host__ __device__ inline void mrg_apply(const uint32_t* M, uint32_t* s) {
     uint32_t r[6];
