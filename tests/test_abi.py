@@ -60,6 +60,7 @@ int main(void) {
   printf("%zu %zu %zu\n", offsetof(prisma_params_t, engine), sizeof(prisma_plan_t), offsetof(prisma_plan_t, engine));
   printf("%zu %zu %zu %zu\n", offsetof(prisma_params_t, signaling_type), offsetof(prisma_params_t, big_signaling),
          offsetof(prisma_params_t, sync_step_s), offsetof(prisma_params_t, big_signaling_bytes));
+  printf("%zu %zu\n", offsetof(prisma_params_t, rng_mode), offsetof(prisma_params_t, rng_stream_offset));
   return 0;
 }
 '''
@@ -85,6 +86,8 @@ def test_ctypes_layouts_match_header():
     sig = list(map(int, lines[3].split()))
     assert sig == [getattr(engine._Params, k).offset for k in
                    ("signaling_type", "big_signaling", "sync_step_s", "big_signaling_bytes")]
+    rng = list(map(int, lines[4].split()))
+    assert rng == [engine._Params.rng_mode.offset, engine._Params.rng_stream_offset.offset]
 
 
 def test_engine_refuses_without_gpu():
