@@ -14,7 +14,8 @@ import os
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "prisma_amd", "csrc")
 
-ENGINE_SOURCES = ["prisma_engine.hip", "prisma_engine_lite.hip", "prisma_engine_mem.hip"]
+ENGINE_SOURCES = ["prisma_engine.hip", "prisma_engine_mlp.hip", "prisma_engine_lite.hip", "prisma_engine_lite_mlp.hip",
+                  "prisma_engine_mem.hip"]
 ENGINE_HEADERS = ["engine_core.h", "engine_layout.h", "numerics.h", "step_kernel.h", "mrg32k3a.h"]
 HIPCC_FLAGS = ["--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC", "-std=c++17",
                # the per-replica counters are bumped by lane 0 only: the atomic optimizer's

@@ -518,6 +518,7 @@ __device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, const Ho
 }
 
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v);
+__device__ __forceinline__ uint32_t wave_umin_fast(uint32_t v);
 
 // Elided completions.  A transmit completion that finds its queue empty only clears
 // `busy` (point-to-point-net-device.cc:305-336: TransmitComplete with no packet left
@@ -933,6 +934,7 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
 #endif
     // ExecuteActions (packet-routing-gym.cc:203-208): the --train echo goes first
     if (echo_link != kNoLink) send_echo(S, R, H, echo_link, uid, last);
+    v = rfl(v);                                     // (scalar loads of the row pointers)
     int r0 = t_ovrow(S, v), deg = t_ovrow(S, v + 1) - r0;
     uint32_t status;
     if (action >= 0 && action < deg) {
@@ -1220,6 +1222,7 @@ __device__ __forceinline__ void mlp_preload(MlpPre& M, const float* __restrict__
 // them in registers
 __device__ __forceinline__ void mlp_preload_node(MlpPre1& M, const Sim& S, uint32_t v, uint32_t dst, bool has_w1) {
     const int lane = S.lane;
+    v = rfl(v);                  // uniform: the row pointers come from scalar loads
     const int D = S.lv.max_deg();
     const float* __restrict__ RP1 = S.mlp_rp + (size_t)v * mlp_rp_node_floats(D);
     const float* __restrict__ RP = RP1 + mlp_rp_l1_floats(D);
@@ -1254,11 +1257,47 @@ __device__ __forceinline__ float mlp_dense64_pre(const Sim& S, const float4 (&w)
 // one-hot input: obs[0] (the destination's overlay index, lane 0 of obs_reg)
 __device__ __forceinline__ float rdlf(float x, uint32_t k) { return __uint_as_float(rdl(__float_as_uint(x), k)); }
 
+// x of lanes 1..n summed in lane order (((0 + x1) + x2) + ...), four readlanes issued per
+// step; a lane past n contributes -0.0f, the identity of round-to-nearest addition (the sum
+// starts at +0 and so is never -0), so the result equals the one-add-per-lane loop's
+__device__ __forceinline__ float lane_sum_ordered(float x, int n) {
+    float sum = 0.0f;
+    for (int k0 = 0; k0 < n; k0 += 4) {
+        float v[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) v[i] = (k0 + i < n) ? rdlf(x, (uint32_t)(k0 + i + 1) & 63u) : -0.0f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) sum = __fadd_rn(sum, v[i]);
+    }
+    return sum;
+}
+
+// tf.argmin over q of lanes 0..n-1, the first minimum (learner.py:145): the result of
+// `best = 0; for a in 1..n-1: if q[a] < q[best]: best = a`, as one DPP reduction of an
+// order-preserving key (+0 and -0 equal; a NaN past lane 0 never wins; a NaN in lane 0 wins,
+// since nothing compares below it) and a ballot for the lowest lane among equal keys
+__device__ __forceinline__ int lane_argmin_first(float q, int n) {
+    const int lane = (int)threadIdx.x;
+    uint32_t u = __float_as_uint(q);
+    u = (u << 1) == 0u ? 0u : u;                                    // -0 -> +0
+    uint32_t key = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    key = (lane >= n || (q != q)) ? 0xffffffffu : key;
+    const uint32_t kmin = wave_umin_fast(key);
+    const float q0 = rdlf(q, 0);
+    if (q0 != q0) return 0;
+    return (int)__builtin_ctzll(__ballot(key == kmin));
+}
+
 template <int B, bool PRE = false>
 __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs_reg, const MlpPre1& P1) {
     const LV& L = S.lv;
     const int lane = S.lane;
     const int N = L.N(), D = L.max_deg();
+    // v (and with it deg) uniform: the row pointers then come from scalar loads.  Passed through
+    // the decision record the compiler had lost that, loaded deg with vector loads and waited
+    // for them behind the layer 3-4 weight stream (s_waitcnt vmcnt), and ran the LayerNorm
+    // sums as exec-mask loops
+    v = rfl(v);
     const float* __restrict__ W1 = S.mlp;
     const float* __restrict__ RP1 = S.mlp_rp + (size_t)v * mlp_rp_node_floats(D);
     const float* __restrict__ RP = RP1 + mlp_rp_l1_floats(D);
@@ -1296,14 +1335,18 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     }
     // LayerNormalization of the deg buffer values (population variance, epsilon 1e-3):
     // lane k+1 holds buffer value k; sums run in k order through readlanes
+    // (the memory-resident engine's single wave per SIMD gains from the 4-wide sums and the
+    // DPP argmin below; the register-resident MLP instances lost 1 % with them, A/B on GEANT)
     const float xf = (float)obs_reg;
     float sum = 0.0f;
-    for (int k = 0; k < deg; ++k) sum = __fadd_rn(sum, rdlf(xf, (uint32_t)(k + 1)));
+    if constexpr (B == kMlpAll) sum = lane_sum_ordered(xf, deg);
+    else for (int k = 0; k < deg; ++k) sum = __fadd_rn(sum, rdlf(xf, (uint32_t)(k + 1)));
     const float mean = __fdiv_rn(sum, (float)deg);
     const float dv = __fsub_rn(xf, mean);
     const float sq = __fmul_rn(dv, dv);
     float var = 0.0f;
-    for (int k = 0; k < deg; ++k) var = __fadd_rn(var, rdlf(sq, (uint32_t)(k + 1)));
+    if constexpr (B == kMlpAll) var = lane_sum_ordered(sq, deg);
+    else for (int k = 0; k < deg; ++k) var = __fadd_rn(var, rdlf(sq, (uint32_t)(k + 1)));
     var = __fdiv_rn(var, (float)deg);
     const float den = __fsqrt_rn(__fadd_rn(var, 1e-3f));
     const float xn = __fdiv_rn(dv, den);                          // lane k+1: normalised value k
@@ -1351,10 +1394,14 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     __builtin_amdgcn_wave_barrier();
     // tf.argmin: first minimum (learner.py:145)
     int best = 0;
-    float bq = __uint_as_float(rdl(__float_as_uint(q), 0));
-    for (int a = 1; a < deg; ++a) {
-        const float qa = __uint_as_float(rdl(__float_as_uint(q), (uint32_t)a));
-        if (qa < bq) { bq = qa; best = a; }
+    if constexpr (B == kMlpAll) {
+        best = lane_argmin_first(q, deg);
+    } else {
+        float bq = __uint_as_float(rdl(__float_as_uint(q), 0));
+        for (int a = 1; a < deg; ++a) {
+            const float qa = __uint_as_float(rdl(__float_as_uint(q), (uint32_t)a));
+            if (qa < bq) { bq = qa; best = a; }
+        }
     }
     TM_MLP(3);
     return best;

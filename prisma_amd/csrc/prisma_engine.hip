@@ -106,10 +106,13 @@ __global__ void __launch_bounds__(64) prisma_reset_kernel_t(KParams P) {
     }
 }
 
-// step kernels (step_kernel.h): the instances with the --train / notify_dest code paths
-// are compiled here, the ones without them in prisma_engine_lite.hip
-const void* prisma_pick_step_lite(int fs, int ls, bool mlp, bool tun);
-static const void* pick_step_ctrl(int fs, int ls, bool mlp, bool tun) { return pick_step<true>(fs, ls, mlp, tun); }
+// step kernels (step_kernel.h): the table-policy instances with the --train / notify_dest
+// code paths are compiled here, the in-kernel DQN-buffer ones in prisma_engine_mlp.hip, the
+// ones without those paths in prisma_engine_lite.hip / prisma_engine_lite_mlp.hip
+const void* prisma_pick_step_lite(int fs, int ls, bool tun);
+const void* prisma_pick_step_lite_mlp(int fs, int ls, bool tun);
+const void* prisma_pick_step_ctrl_mlp(int fs, int ls, bool tun);
+static const void* pick_step_ctrl(int fs, int ls, bool tun) { return pick_step<true, false>(fs, ls, tun); }
 
 template <int FS, int LS> const void* reset_kernel() { return (const void*)prisma_reset_kernel_t<FS, LS>; }
 static const void* pick_reset(int fs, int ls) {
@@ -224,15 +227,7 @@ extern "C" int prisma_abi_version(void) { return PRISMA_ABI_VERSION; }
 static const char k_build_id[] = "PRISMA_BUILD_ID=" PRISMA_BUILD_ID;
 extern "C" const char* prisma_build_id(void) { return k_build_id + 16; }
 
-#if PRISMA_TIMING
-// diagnostic build only: read and clear the per-phase cycle totals
-extern "C" int prisma_debug_timing(unsigned long long* out16) {
-    if (!HIP_OK(hipDeviceSynchronize()) ||
-        !HIP_OK(hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prisma_timing), 32 * sizeof(unsigned long long)))) return -1;
-    unsigned long long z[32] = {0};
-    return HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_timing), z, sizeof(z))) ? 0 : -1;
-}
-#endif
+PRISMA_TU_TIMING(prisma_debug_timing)
 extern "C" const char* prisma_last_error(void) { return g_err.c_str(); }
 
 static uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
@@ -964,9 +959,10 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
         // instances that need them
         const bool ctrl = L.train || L.notify_dest || L.rng_mode;
         auto pick = ctrl ? pick_step_ctrl : prisma_pick_step_lite;
-        e->k_step = pick(L.FS, L.LS, false, L.tunnels != 0u);
+        auto pick_mlp = ctrl ? prisma_pick_step_ctrl_mlp : prisma_pick_step_lite_mlp;
+        e->k_step = pick(L.FS, L.LS, L.tunnels != 0u);
         e->k_reset = pick_reset(L.FS, L.LS);
-        e->k_step_mlp = pick(L.FS, L.LS, true, L.tunnels != 0u);
+        e->k_step_mlp = pick_mlp(L.FS, L.LS, L.tunnels != 0u);
     }
     (void)hipFuncSetAttribute(e->k_step_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_mlp_bytes);
     (void)hipFuncSetAttribute(e->k_step, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);

@@ -48,7 +48,7 @@ __device__ __forceinline__ uint32_t leaf_of(const MemSt& R, uint32_t code) {
 // uniform (t, seq, code) minimum over the lanes (lowest (t, seq); seqs are unique
 // among finite keys, so the winner is unique unless every key is infinite)
 struct Key { int64_t t; uint32_t s, c; };
-__device__ __forceinline__ Key wave_min_key(int64_t t, uint32_t s, uint32_t c) {
+__device__ __forceinline__ Key wave_min_key_exact(int64_t t, uint32_t s, uint32_t c) {
     Key k;
     k.t = wave_min_i64(t);
     const bool tie = (t == k.t);
@@ -57,6 +57,29 @@ __device__ __forceinline__ Key wave_min_key(int64_t t, uint32_t s, uint32_t c) {
     if ((tied & (tied - 1)) == 0) {
         win = (uint32_t)__builtin_ctzll(tied);
     } else {
+        const uint32_t smin = wave_umin_fast(tie ? s : 0xffffffffu);
+        win = (uint32_t)__builtin_ctzll(__ballot(tie && s == smin));
+    }
+    k.s = rdl(s, win);
+    k.c = rdl(c, win);
+    return k;
+}
+// The same minimum when every key is >= now (pending events, infinite keys): reduced as
+// 32-bit offsets from the clock, saturated at 2^32-1, with one fused v_min_u32_dpp per step
+// (the register-resident engine's select_event) instead of the 64-bit DPP compare/select
+// chain; if every key saturates, the exact 64-bit reduction runs.
+__device__ __forceinline__ Key wave_min_key(int64_t t, uint32_t s, uint32_t c, int64_t now) {
+    const uint32_t o = sat_offset(t, now);
+    const uint32_t omin = wave_umin_fast(o);
+    if (omin == 0xffffffffu) return wave_min_key_exact(t, s, c);
+    Key k;
+    k.t = now + (int64_t)omin;
+    const bool tie = (o == omin);
+    const uint64_t tied = __ballot(tie);
+    uint32_t win;
+    if ((tied & (tied - 1)) == 0) {
+        win = (uint32_t)__builtin_ctzll(tied);
+    } else {                                                        // same-ns keys: seq order
         const uint32_t smin = wave_umin_fast(tie ? s : 0xffffffffu);
         win = (uint32_t)__builtin_ctzll(__ballot(tie && s == smin));
     }
@@ -96,10 +119,10 @@ __device__ __forceinline__ Key block_min(const Sim& S, const MemSt& R, uint32_t 
         s = k.z;
         c = (K_FLOW << 28) | (leaf - R.L);
     }
-    return wave_min_key(t, s, c);
+    return wave_min_key(t, s, c, now);
 }
 // minimum of level-1 group g (64 block minima)
-__device__ __forceinline__ Key group_min(const Sim& S, const MemSt& R, uint32_t g) {
+__device__ __forceinline__ Key group_min(const Sim& S, const MemSt& R, uint32_t g, int64_t now) {
     const uint32_t i = g * 64u + (uint32_t)S.lane;
     int64_t t = kInf;
     uint32_t s = 0xffffffffu, c = 0u;
@@ -109,7 +132,7 @@ __device__ __forceinline__ Key group_min(const Sim& S, const MemSt& R, uint32_t 
         s = k.z;
         c = k.w;
     }
-    return wave_min_key(t, s, c);
+    return wave_min_key(t, s, c, now);
 }
 
 // block_min of the cached flow block, with `leaf` holding the new key (t, seq, code); link
@@ -134,7 +157,7 @@ __device__ __forceinline__ Key block_min_cached(const Sim& S, const MemSt& R, ui
         s = R.fblk.z;
         c = (K_FLOW << 28) | (li - R.L);
     }
-    return wave_min_key(t, s, c);
+    return wave_min_key(t, s, c, now);
 }
 
 // Source `leaf`'s next event changed to (t, seq): store its key and repair the two
@@ -165,7 +188,7 @@ __device__ __forceinline__ void tree_touch(const Sim& S, MemSt& R, const Hot& H,
     if (key_less(nb.t, nb.s, cg.t, cg.s)) {
         ng = nb;
     } else if (leaf_of(R, cg.c) == leaf_of(R, cur.c)) {
-        ng = group_min(S, R, g);
+        ng = group_min(S, R, g, H.now);
     } else {
         return;
     }
@@ -317,7 +340,7 @@ __device__ __forceinline__ void select_event(const Sim& S, const MemSt& R, const
         c = k.w;
     }
     if (lane == 0 && key_less(H.ping_t, H.ping_seq, t, s)) { t = H.ping_t; s = H.ping_seq; c = K_PING << 28; }
-    const Key k = wave_min_key(t, s, c);
+    const Key k = wave_min_key(t, s, c, H.now);
     bt = k.t;
     bc = k.c;
     bs = k.s;
@@ -421,7 +444,7 @@ __device__ __forceinline__ void init_replica(Sim& S, MemSt& R, Hot& H, uint32_t 
     __syncthreads();
     for (uint32_t b = 0; b < R.n1; ++b) lds_put_key(S, &R.lv1[b], block_min(S, R, b, 0));
     __syncthreads();
-    for (uint32_t g = 0; g < R.n2; ++g) lds_put_key(S, &R.lv2[g], group_min(S, R, g));
+    for (uint32_t g = 0; g < R.n2; ++g) lds_put_key(S, &R.lv2[g], group_min(S, R, g, 0));
     H.now = 0;
     H.ping_t = L.ping_period();
     H.ping_seq = 0;

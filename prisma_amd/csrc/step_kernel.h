@@ -61,24 +61,40 @@ prisma_step_kernel_t(KParams P) {
 }
 
 // instantiations: flow slots FS in {1,2,4,8} (F <= 512), link slots LS in {1,2,4} (L <= 256)
-template <int FS, int LS, bool CTRL> const void* step_kernel(bool mlp, bool tun) {
-    if (mlp) return tun ? (const void*)prisma_step_kernel_t<FS, LS, true, true, CTRL>
-                        : (const void*)prisma_step_kernel_t<FS, LS, true, false, CTRL>;
-    return tun ? (const void*)prisma_step_kernel_t<FS, LS, false, true, CTRL>
-               : (const void*)prisma_step_kernel_t<FS, LS, false, false, CTRL>;
+template <int FS, int LS, bool CTRL, bool MLP> const void* step_kernel(bool tun) {
+    return tun ? (const void*)prisma_step_kernel_t<FS, LS, MLP, true, CTRL>
+               : (const void*)prisma_step_kernel_t<FS, LS, MLP, false, CTRL>;
 }
 
-// tun: tunnelled-overlay instance (identity overlays run code without the tunnel paths)
-template <bool CTRL>
-static const void* pick_step(int fs, int ls, bool mlp, bool tun) {
+// tun: tunnelled-overlay instance (identity overlays run code without the tunnel paths).
+// One translation unit per (CTRL, MLP) instance set, so the four sets compile in parallel:
+// prisma_engine.hip (CTRL, tables), prisma_engine_mlp.hip (CTRL, MLP), prisma_engine_lite.hip
+// and prisma_engine_lite_mlp.hip (without the ctrl paths)
+template <bool CTRL, bool MLP>
+static const void* pick_step(int fs, int ls, bool tun) {
 #ifdef PRISMA_DEV_HEADLINE
     // register-allocation experiments only: compile the headline instance alone
-    return (!CTRL && fs == 2 && ls == 1 && !mlp && !tun) ? (const void*)prisma_step_kernel_t<2, 1, false, false, false>
+    return (!CTRL && !MLP && fs == 2 && ls == 1 && !tun) ? (const void*)prisma_step_kernel_t<2, 1, false, false, false>
                                                          : nullptr;
 #else
-#define PK(F_, L_) if (fs == F_ && ls == L_) return step_kernel<F_, L_, CTRL>(mlp, tun);
+#define PK(F_, L_) if (fs == F_ && ls == L_) return step_kernel<F_, L_, CTRL, MLP>(tun);
     PK(1, 1) PK(1, 2) PK(1, 4) PK(2, 1) PK(2, 2) PK(2, 4) PK(4, 1) PK(4, 2) PK(4, 4) PK(8, 1) PK(8, 2) PK(8, 4)
 #undef PK
     return nullptr;
 #endif
 }
+
+#if PRISMA_TIMING
+// diagnostic build only: read and clear this translation unit's per-phase cycle totals
+// (g_prisma_timing is one copy per translation unit; scripts/timing.py)
+#define PRISMA_TU_TIMING(NAME)                                                                          \
+    extern "C" int NAME(unsigned long long* out32) {                                                    \
+        if (hipDeviceSynchronize() != hipSuccess ||                                                     \
+            hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prisma_timing), 32 * sizeof(unsigned long long)) != \
+                hipSuccess) return -1;                                                                  \
+        unsigned long long z[32] = {0};                                                                 \
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;     \
+    }
+#else
+#define PRISMA_TU_TIMING(NAME)
+#endif

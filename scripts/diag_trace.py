@@ -15,7 +15,9 @@ CSRC = os.path.join(ROOT, "prisma_amd", "csrc")
 if sys.argv[1] == "build":
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     objs = []
-    for f in ("prisma_engine.hip", "prisma_engine_lite.hip", "prisma_engine_mem.hip"):
+    sys.path.insert(0, ROOT)
+    from prisma_amd import buildid
+    for f in buildid.ENGINE_SOURCES:
         o = os.path.join(os.path.dirname(LIB), f + ".trace.o")
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC",
                                "-std=c++17", "-DPRISMA_TRACE=1", "-c", "-o", o, os.path.join(CSRC, f)])

@@ -16,7 +16,9 @@ NAMES = ["select", "arrive", "decision", "complete", "flow", "ping_round", "dec:
 if sys.argv[1] == "build":
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     objs = []
-    for f in ("prisma_engine.hip", "prisma_engine_lite.hip", "prisma_engine_mem.hip"):
+    sys.path.insert(0, ROOT)
+    from prisma_amd import buildid
+    for f in buildid.ENGINE_SOURCES:
         o = os.path.join(os.path.dirname(LIB), f + ".timing.o")
         subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC",
                                "-std=c++17", "-DPRISMA_TIMING=1", "-c", "-o", o,
@@ -43,8 +45,13 @@ eng = PrismaEngine(topo, engine_params(topo, sim_time_s=60.0, ping_as_obs=PAO, a
                                       log_capacity=65536 if topo.n_links > 256 else 8192), R)
 lib = load_library()
 # the kernels without the --train / notify_dest paths live in their own translation unit
-timing = lib.prisma_debug_timing_mem if eng.engine_kind == 2 else (
-    lib.prisma_debug_timing if ", true>" in eng.kernel_name else lib.prisma_debug_timing_lite)
+# (one translation unit per instance set: step_kernel.h; kernel name <FS, LS, MLP, TUN, CTRL>)
+_kname = eng.kernel_name_mlp if POLICY == "dqn_buffer" else eng.kernel_name
+_targs = [a.strip() for a in _kname.split("<")[-1].rstrip(">").split(",")]
+timing = lib.prisma_debug_timing_mem if eng.engine_kind == 2 else getattr(
+    lib, {("false", "true"): "prisma_debug_timing", ("true", "true"): "prisma_debug_timing_mlp",
+          ("false", "false"): "prisma_debug_timing_lite",
+          ("true", "false"): "prisma_debug_timing_lite_mlp"}[(_targs[2], _targs[4])])
 timing.argtypes = [C.c_void_p]
 if POLICY == "dqn_buffer":
     table = StackedQNet(topo, "buffer", seed=1234, device="cuda").pack()
