@@ -657,6 +657,7 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
                                                uint32_t x) {
     const LV& L = S.lv;
     const bool sw = l < (uint32_t)L.E();
+    x = rfl(x);                  // uniform entry: its class indexes the topology image with a scalar load
     // register-resident engine: a switch link's tx time by entry class from the topology image
     // (--train instances: an echo's by link, sized by its sender)
     // (memory-resident: by entry type from the scenario constants; --train instances: echoes by
@@ -1210,10 +1211,14 @@ __device__ __forceinline__ void mlp_preload(MlpPre& M, const float* __restrict__
     }
 #pragma unroll
     for (int c = 0; c < 16; ++c) M.w3[c] = W3[c * 64 + lane];
+    // layer 4: lanes past deg read lane 0's weights (their outputs are discarded), so every
+    // load of the stream is unconditional and the in-order load counter can be waited on
+    // exactly (exec-masked loads made the compiler wait for layer 3's weights in layer 1)
+    const int l4 = lane < deg ? lane : 0;
 #pragma unroll
-    for (int c = 0; c < 16; ++c) M.w4[c] = lane < deg ? W4[c * D + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int c = 0; c < 16; ++c) M.w4[c] = W4[c * D + l4];
     M.b3 = RP[mlp_rp_layer_floats(64) + 64 * 64 + lane];
-    M.b4 = lane < deg ? RP[2 * mlp_rp_layer_floats(64) + 64 * D + lane] : 0.0f;
+    M.b4 = RP[2 * mlp_rp_layer_floats(64) + 64 * D + l4];
 }
 
 // layers 1-2 of a decision at node v (the one-hot row too when the destination dst is
@@ -1320,6 +1325,18 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     float w1v;
     if (PRE && P1.has_w1) w1v = P1.w1v;
     else w1v = (lane < 32) ? W1[((int)v * N + (int)dst) * 32 + j32] : 0.0f;
+    // memory-resident engine: buffer-branch chunks 4-7 (degrees 17-32) are loaded here, BEFORE
+    // the layer 3-4 stream: the load counter is in order, so a chunk loaded inside layer 1
+    // made layer 1 wait for the whole stream (and the compiler, unable to count the loop's
+    // loads, waited for everything before layer 2)
+    float4 wx[4];
+    if constexpr (B == kMlpAll) {
+        // (always issued, chunk 0 again past the node's degree: no branch for the scheduler to
+        // hoist the stream's loads above)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) wx[c] = Wb4[((c + 4 < nck) ? c + 4 : 0) * 32 + j32];
+        __builtin_amdgcn_sched_barrier(0);
+    }
     MlpPre M;
     if constexpr (B == kMlpAll) mlp_preload(M, RP, lane, D, deg, !PRE);   // PRE: layer 2 came with the arrival
     float b1v;
@@ -1354,18 +1371,29 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     // buffers dot product runs with every lane active (lanes 0-31 discard it): its
     // readlanes read xn from lanes 1..deg, which must not sit in an inactive branch.
     float acc = 0.0f;
-    for (int c = 0; c < nck; ++c) {
-        float4 w;
-        if (c < 4) {
-            w = (c == 0) ? wb[0] : (c == 1) ? wb[1] : (c == 2) ? wb[2] : wb[3];
-        } else {
-            w = Wb4[c * 32 + j32];
-        }
+    auto chunk = [&](int c, const float4& w) {
         const int k = 4 * c;
         acc = __builtin_fmaf(rdlf(xn, (uint32_t)(k + 1)), w.x, acc);
         if (k + 1 < deg) acc = __builtin_fmaf(rdlf(xn, (uint32_t)(k + 2)), w.y, acc);
         if (k + 2 < deg) acc = __builtin_fmaf(rdlf(xn, (uint32_t)(k + 3)), w.z, acc);
         if (k + 3 < deg) acc = __builtin_fmaf(rdlf(xn, (uint32_t)(k + 4)), w.w, acc);
+    };
+    if constexpr (B == kMlpAll) {
+        // chunks named at compile time (a runtime-indexed select over wb/wx put them on the stack)
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+            if (c < nck) chunk(c, c < 4 ? wb[c & 3] : wx[c & 3]);
+        for (int c = 8; c < nck; ++c) chunk(c, Wb4[c * 32 + j32]);
+    } else {
+        for (int c = 0; c < nck; ++c) {
+            float4 w;
+            if (c < 4) {
+                w = (c == 0) ? wb[0] : (c == 1) ? wb[1] : (c == 2) ? wb[2] : wb[3];
+            } else {
+                w = Wb4[c * 32 + j32];
+            }
+            chunk(c, w);
+        }
     }
     float h = det_elu(__fadd_rn(lane < 32 ? w1v : acc, b1v));
     S.hbuf[lane] = h;

@@ -14,17 +14,27 @@ LIB = os.path.join(ROOT, "prisma_amd", "_ablate", "libprisma_amd_timing.so")
 NAMES = ["select", "arrive", "decision", "complete", "flow", "ping_round", "dec:send", "dec:record"]
 
 if sys.argv[1] == "build":
+    # `build mem`: only the memory-resident engine's translation unit with the timing probes,
+    # the others from the in-tree objects of the last build_engine (same sources)
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    objs = []
     sys.path.insert(0, ROOT)
     from prisma_amd import buildid
+    only = sys.argv[2:] and sys.argv[2] == "mem"
+    objs, procs = [], []
     for f in buildid.ENGINE_SOURCES:
+        if only and f != "prisma_engine_mem.hip":
+            objs.append(os.path.join(ROOT, "prisma_amd", "csrc", os.path.splitext(f)[0] + ".o"))
+            continue
         o = os.path.join(os.path.dirname(LIB), f + ".timing.o")
-        subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-ffp-contract=off", "-fPIC",
-                               "-std=c++17", "-DPRISMA_TIMING=1", "-c", "-o", o,
-                               os.path.join(ROOT, "prisma_amd", "csrc", f)])
+        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", *buildid.HIPCC_FLAGS, "-DPRISMA_TIMING=1", "-c", "-o", o,
+                                       os.path.join(ROOT, "prisma_amd", "csrc", f)]))
         objs.append(o)
+    if any(p.wait() != 0 for p in procs):
+        sys.exit("hipcc failed")
     subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB, *objs])
+    for o in objs:
+        if o.endswith(".timing.o"):
+            os.remove(o)
     sys.exit(0)
 
 os.environ["PRISMA_LIB"] = LIB
