@@ -52,6 +52,9 @@ static __device__ unsigned int g_prisma_trace_n[8];
 #if PRISMA_TIMING
 static __device__ unsigned long long g_prisma_timing[32];   // one copy per engine (translation unit); 16-19: mlp_action phases
 #define TM_NOW() ((uint64_t)__builtin_amdgcn_s_memtime())
+#define TM_FLOW(i) do { const uint64_t t_ = TM_NOW(); S.tflow[i] += t_ - S.tfl; S.tfl = t_; } while (0)
+#else
+#define TM_FLOW(i) do { } while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -318,6 +321,7 @@ struct Sim {
 #if PRISMA_TIMING
     mutable uint64_t tsub[2], tlast;             // sub-phase cycles inside apply_decision
     mutable uint64_t tmlp[4];                    // mlp_action phases (timing build)
+    mutable uint64_t tflow[4], tfl;              // memory-resident on_flow phases (timing build)
 #endif
 };
 
@@ -1081,7 +1085,9 @@ __device__ __forceinline__ void flow_next(const Sim& S, RS& R, Hot& H, uint32_t 
     double U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
     double delay = -t_fmean(S, f) * det_log(U);
     int64_t t = H.now + sec_to_ns(delay);
+    if constexpr (RS::kMem) TM_FLOW(2);
     flow_set(S, R, H, f, t, H.seq++, draw + 1);
+    if constexpr (RS::kMem) TM_FLOW(3);
 }
 
 // The BigSignalingGeneratorApplications (big-signaling-application.cc:224-309), all in flow
@@ -1112,16 +1118,21 @@ __device__ __forceinline__ void on_flow(const Sim& S, RS& R, Hot& H, uint32_t f)
     // memory-resident engine: the access link's record is fetched first, so its load and the
     // flow block's are in flight together (one HBM round trip)
     uint32_t draw;
+#if PRISMA_TIMING
+    S.tfl = TM_NOW();
+#endif
     if constexpr (RS::kMem) {
         if (S.ctrl && f >= (uint32_t)S.lv.F()) { on_bsig(S, R, H, f); return; }
         const uint32_t acc = (uint32_t)S.lv.E() + (uint32_t)t_fsrc(S, f);
         const LinkV k = link_get(R, acc);
         draw = flow_draw(S, R, f);
+        TM_FLOW(0);
         if (draw != 0) {                                            // SendPacket :297-358
             const uint32_t par = (uint32_t)(TSEC(H.now)) & 1u;          // start second (its parity)
             link_send_k(S, R, H, acc, f_make((uint32_t)t_fdst(S, f), par, H.uid & kUidMask), k);
             H.uid++;
         }
+        TM_FLOW(1);
     } else {
         if (S.ctrl && f >= (uint32_t)S.lv.F()) { on_bsig(S, R, H, f); return; }
         draw = flow_draw(S, R, f);
@@ -2062,6 +2073,7 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
     uint64_t tm_a = 0, tm_b = 0;
     S.tsub[0] = 0; S.tsub[1] = 0; S.tlast = 0;
     S.tmlp[0] = 0; S.tmlp[1] = 0; S.tmlp[2] = 0; S.tmlp[3] = 0;
+    S.tflow[0] = 0; S.tflow[1] = 0; S.tflow[2] = 0; S.tflow[3] = 0; S.tfl = 0;
 #define TM_MARK(i) do { tm_b = TM_NOW(); tm_acc[i] += tm_b - tm_a; tm_cnt[i]++; tm_a = tm_b; } while (0)
 #else
 #define TM_MARK(i) do { } while (0)
@@ -2147,6 +2159,7 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
             atomicAdd(&g_prisma_timing[8 + i], (unsigned long long)tm_cnt[i]);
         }
         for (int i = 0; i < 4; ++i) atomicAdd(&g_prisma_timing[16 + i], (unsigned long long)S.tmlp[i]);
+        for (int i = 0; i < 4; ++i) atomicAdd(&g_prisma_timing[20 + i], (unsigned long long)S.tflow[i]);
     }
 #endif
     if (!H.error) lazy_resolve(S, R, H, false);      // elided completions up to where the launch stopped

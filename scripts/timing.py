@@ -88,3 +88,7 @@ if buf[16]:
     nd = buf[8 + 2]
     for i, nm in enumerate(["mlp:ln+l1", "mlp:l2", "mlp:l3", "mlp:l4+argmin"]):
         print(f"  {nm:13s} cyc/decision={buf[16 + i] / max(1, nd):8.0f}")
+if buf[20]:
+    nf = buf[8 + 4]
+    for i, nm in enumerate(["flow:record+block", "flow:send", "flow:draw", "flow:tree"]):
+        print(f"  {nm:17s} cyc/flow={buf[20 + i] / max(1, nf):8.0f}")
