@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PRISMA_ABI_VERSION 8
+#define PRISMA_ABI_VERSION 9
 
 /* status codes */
 #define PRISMA_OK              0
@@ -193,7 +193,10 @@ typedef struct prisma_params {
                                    on (sim.cc:634-647, big-signaling-
                                    application.cc:224-309)                 */
     float    sync_step_s;       /* syncStep: seconds per NN copy   [1.0]   */
-    uint32_t big_signaling_bytes; /* bigSignalingSize: NN bytes   [35328]  */
+    uint32_t big_signaling_bytes; /* bigSignalingSize: NN bytes; sim.cc's own
+                                     default is 35328, the CLI's (argument_parser.py:74)
+                                     512 = one segment per NN; prisma_amd's
+                                     config.engine_params passes 512 */
     /* ---- ABI 8 ---- */
     uint32_t rng_mode;          /* PRISMA_RNG_*                    [0]     */
     uint32_t rng_stream_offset; /* PRISMA_RNG_NS3: streams ns-3 itself
@@ -346,6 +349,26 @@ int prisma_copy_counters(prisma_env_t* env, void* dst_device, void* stream);
  * keeps dec[i] within the last log_capacity decisions of that replica. */
 int prisma_gather_records(prisma_env_t* env, const int32_t* replica, const uint32_t* dec,
                           int32_t n, void* dst_device, void* stream);
+
+/* Active-replica compaction (ABI 9) for a batched external policy, which then
+ * evaluates only the replicas with a pending decision -- the reference's
+ * Forwarder steps only the nodes that were notified (ns3env.py:417-423,
+ * forwarder.py:135-195).  From the outputs of a prisma_step (mask [R], obs
+ * [R][obs_width], node [R]; obs / node may be NULL): ids_out[0..count) = the
+ * replica ids with mask 1 in ascending order, obs_packed[i] = obs row of
+ * ids_out[i], node_packed[i] = its deciding node, count_out[0] = count (all
+ * device int32; obs_packed / node_packed may be NULL).  A wavefront ballot and
+ * a prefix sum of the wave totals; one launch on `stream`, no host sync. */
+int prisma_compact_pending(prisma_env_t* env, const uint8_t* mask, const int32_t* obs,
+                           const int32_t* node, int32_t* ids_out, int32_t* obs_packed,
+                           int32_t* node_packed, int32_t* count_out, void* stream);
+
+/* The inverse for the actions: actions_out[r] = fill for every replica, then
+ * actions_out[ids[i]] = packed_actions[i] for i < count[0] (device arrays);
+ * actions_out then feeds prisma_step. */
+int prisma_expand_actions(prisma_env_t* env, const int32_t* ids, const int32_t* count,
+                          const int32_t* packed_actions, int32_t fill, int32_t* actions_out,
+                          void* stream);
 
 /* Bytes of per-replica state (the LDS image) and LDS bytes per workgroup. */
 int prisma_state_bytes(prisma_env_t* env, uint32_t* state_bytes,

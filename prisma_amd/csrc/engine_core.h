@@ -1270,6 +1270,75 @@ __device__ __forceinline__ float mlp_dense64_pre(const Sim& S, const float4 (&w)
     return __fadd_rn(acc, b);
 }
 
+// Layers 2-4 of the register-resident instances with the weight loads one batch ahead: batch
+// t+1's loads (across layer boundaries too) are issued before batch t's FMAs, so each L2 round
+// trip overlaps a batch of FMAs instead of standing alone.  Per lane the same operations in
+// the same order as mlp_dense64 for each layer (bit-identical); layer 4's lanes past deg read
+// lane 0's weights and their outputs are discarded by the caller.
+#ifndef PRISMA_MLP_PIPE
+#define PRISMA_MLP_PIPE 1
+#endif
+template <int B>
+__device__ __forceinline__ void mlp_l2_first(float4 (&w0)[B], const float* __restrict__ RP, int lane) {
+    const float4* __restrict__ W4 = (const float4*)RP;
+#pragma unroll
+    for (int c = 0; c < B; ++c) w0[c] = W4[c * 64 + lane];
+}
+// w0: layer 2's first batch, issued by the caller before layer 1 (mlp_l2_first) when EARLY
+// (the 256-VGPR instances: config 4 +1.2 % over issuing it here; the 128-VGPR ones lose 0.5 %)
+template <int B, bool EARLY>
+__device__ __forceinline__ float mlp_l234_pipe(const Sim& S, const float* __restrict__ RP, int lane, int D, int deg,
+                                               const float4 (&w0)[B]) {
+    constexpr int NB = 16 / B, T = 3 * NB;
+    const float4* __restrict__ hb = (const float4*)S.hbuf;
+    const int l4 = lane < deg ? lane : 0;
+    float4 w[2][B];
+    float bias[3];
+    if constexpr (EARLY) {
+#pragma unroll
+        for (int c = 0; c < B; ++c) w[0][c] = w0[c];
+    }
+    auto issue = [&](int t) {
+        const int Lk = t / NB, c0 = (t % NB) * B;
+        const int units = Lk < 2 ? 64 : D, ln = Lk < 2 ? lane : l4;
+        const float* __restrict__ Wl = RP + Lk * mlp_rp_layer_floats(64);
+        const float4* __restrict__ W4 = (const float4*)Wl;
+#pragma unroll
+        for (int c = 0; c < B; ++c) w[t & 1][c] = W4[(c0 + c) * units + ln];
+        if (t % NB == NB - 1) bias[Lk] = Wl[64 * units + ln];
+    };
+    float acc = 0.0f, q = 0.0f;
+    if constexpr (!EARLY) issue(0);
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        if (t + 1 < T) issue(t + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        const int c0 = (t % NB) * B;
+#pragma unroll
+        for (int c = 0; c < B; ++c) {
+            const float4 h = hb[c0 + c];
+            acc = __builtin_fmaf(h.x, w[t & 1][c].x, acc);
+            acc = __builtin_fmaf(h.y, w[t & 1][c].y, acc);
+            acc = __builtin_fmaf(h.z, w[t & 1][c].z, acc);
+            acc = __builtin_fmaf(h.w, w[t & 1][c].w, acc);
+        }
+        if (t % NB == NB - 1) {
+            const int Lk = t / NB;
+            const float o = det_elu(__fadd_rn(acc, bias[Lk]));
+            acc = 0.0f;
+            if (Lk < 2) {
+                __builtin_amdgcn_wave_barrier();
+                S.hbuf[lane] = o;
+                __builtin_amdgcn_wave_barrier();
+            } else {
+                q = o;
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    return q;
+}
+
 // one-hot input: obs[0] (the destination's overlay index, lane 0 of obs_reg)
 __device__ __forceinline__ float rdlf(float x, uint32_t k) { return __uint_as_float(rdl(__float_as_uint(x), k)); }
 
@@ -1286,6 +1355,18 @@ __device__ __forceinline__ float lane_sum_ordered(float x, int n) {
         for (int i = 0; i < 4; ++i) sum = __fadd_rn(sum, v[i]);
     }
     return sum;
+}
+
+// tf.argmin over q of lanes 0..n-1 as the reference's scan: the first minimum (learner.py:145)
+// (the register-resident instances: their degrees are small)
+__device__ __forceinline__ int lane_argmin_first_seq(float q, int n) {
+    int best = 0;
+    float bq = rdlf(q, 0);
+    for (int a = 1; a < n; ++a) {
+        const float qa = rdlf(q, (uint32_t)a);
+        if (qa < bq) { bq = qa; best = a; }
+    }
+    return best;
 }
 
 // tf.argmin over q of lanes 0..n-1, the first minimum (learner.py:145): the result of
@@ -1361,6 +1442,12 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
 #pragma unroll
         for (int c = 0; c < 4; ++c) wb[c] = (c < nck) ? Wb4[c * 32 + j32] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    // register-resident instances (PRISMA_MLP_PIPE): layer 2's first weights go out now and
+    // load during the LayerNorm and layer 1
+    constexpr int kPipeB = (B != kMlpAll && B >= 2) ? B / 2 : 1;
+    constexpr bool kPipeEarly = B != kMlpAll && B >= 8;
+    float4 w20[kPipeB];
+    if constexpr (kPipeEarly && PRISMA_MLP_PIPE) mlp_l2_first<kPipeB>(w20, RP, lane);
     // LayerNormalization of the deg buffer values (population variance, epsilon 1e-3):
     // lane k+1 holds buffer value k; sums run in k order through readlanes
     // (the memory-resident engine's single wave per SIMD gains from the 4-wide sums and the
@@ -1410,6 +1497,12 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
     TM_MLP(0);
+    if constexpr (B != kMlpAll && PRISMA_MLP_PIPE) {
+        // (half batches double-buffered: the same weight registers as B loads in flight)
+        const float q4 = mlp_l234_pipe<kPipeB, kPipeEarly>(S, RP, lane, D, deg, w20);
+        __builtin_amdgcn_wave_barrier();
+        return lane_argmin_first_seq(q4, deg);
+    }
     if constexpr (PRE) h = det_elu(mlp_dense64_pre(S, P1.w2, P1.b2));
     else if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w2, M.b2));
     else h = det_elu(mlp_dense64<B>(S, RP, lane, 64));
@@ -1432,16 +1525,9 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     }
     __builtin_amdgcn_wave_barrier();
     // tf.argmin: first minimum (learner.py:145)
-    int best = 0;
-    if constexpr (B == kMlpAll) {
-        best = lane_argmin_first(q, deg);
-    } else {
-        float bq = __uint_as_float(rdl(__float_as_uint(q), 0));
-        for (int a = 1; a < deg; ++a) {
-            const float qa = __uint_as_float(rdl(__float_as_uint(q), (uint32_t)a));
-            if (qa < bq) { bq = qa; best = a; }
-        }
-    }
+    int best;
+    if constexpr (B == kMlpAll) best = lane_argmin_first(q, deg);
+    else best = lane_argmin_first_seq(q, deg);
     TM_MLP(3);
     return best;
 }

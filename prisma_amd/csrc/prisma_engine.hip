@@ -140,6 +140,59 @@ extern "C" __global__ void __launch_bounds__(256) prisma_gather_kernel(
     }
 }
 
+// Compaction of the pending replicas of a prisma_step (mask 1) into a dense batch for an
+// external policy (the Forwarder steps only the nodes that were notified, ns3env.py:417-423):
+// one workgroup of 16 waves walks the replicas in chunks of 1 024; each wave ballots its 64
+// mask bytes, a lane's rank among the wave's pending lanes is the popcount of the ballot's
+// lower bits (v_mbcnt), and the 16 wave totals are scanned in LDS. Ids come out ascending.
+constexpr int kCompactThreads = 1024;
+__global__ void __launch_bounds__(kCompactThreads) prisma_compact_kernel(
+        const uint8_t* __restrict__ mask, const int32_t* __restrict__ obs, const int32_t* __restrict__ node, int32_t R,
+        int32_t W, int32_t* __restrict__ ids, int32_t* __restrict__ obs_p, int32_t* __restrict__ node_p,
+        int32_t* __restrict__ count) {
+    __shared__ uint32_t wsum[kCompactThreads / kWave];
+    const uint32_t tid = threadIdx.x, wave = tid / kWave;
+    uint32_t base = 0;
+    for (int32_t c = 0; c < R; c += kCompactThreads) {
+        const int32_t i = c + (int32_t)tid;
+        const bool act = i < R && mask[i] != 0;
+        const uint64_t bal = __ballot(act);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if ((tid & (kWave - 1)) == 0) wsum[wave] = (uint32_t)__builtin_popcountll(bal);
+        __syncthreads();
+        uint32_t off = 0, total = 0;
+        for (uint32_t w = 0; w < kCompactThreads / kWave; ++w) {
+            const uint32_t s = wsum[w];
+            off += w < wave ? s : 0u;
+            total += s;
+        }
+        if (act) {
+            const uint32_t p = base + off + rank;
+            ids[p] = i;
+            if (node_p) node_p[p] = node ? node[i] : -1;
+            if (obs_p)
+                for (int32_t k = 0; k < W; ++k) obs_p[(size_t)p * W + k] = obs[(size_t)i * W + k];
+        }
+        base += total;
+        __syncthreads();                                   // wsum is rewritten by the next chunk
+    }
+    if (tid == 0) count[0] = (int32_t)base;
+}
+
+// The policy's actions for a compacted batch back to one action per replica: fill, then
+// actions[ids[i]] = packed[i] for i < count (one workgroup, so the fill is ordered first).
+__global__ void __launch_bounds__(kCompactThreads) prisma_expand_kernel(
+        const int32_t* __restrict__ ids, const int32_t* __restrict__ count, const int32_t* __restrict__ packed,
+        int32_t R, int32_t fill, int32_t* __restrict__ actions) {
+    for (int32_t i = (int32_t)threadIdx.x; i < R; i += kCompactThreads) actions[i] = fill;
+    __syncthreads();
+    const int32_t n = count[0];
+    for (int32_t i = (int32_t)threadIdx.x; i < n; i += kCompactThreads) {
+        const int32_t r = ids[i];
+        if ((uint32_t)r < (uint32_t)R) actions[r] = packed[i];
+    }
+}
+
 // DQN-buffer weights, row-major [in][out] in the caller's packed buffer (StackedQNet.pack(),
 // models.py:258-306), copied into the interleaved per-node blocks mlp_action reads
 // (engine_core.h, mlp_rp_*): rp[v] = [Wb chunks, bb, b1][W2 chunks, b2][W3 chunks, b3][W4 chunks, b4].
@@ -1122,6 +1175,30 @@ extern "C" int prisma_gather_records(prisma_env_t* e, const int32_t* replica, co
                        (uint32_t*)dst_device);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return set_err(PRISMA_ERR_LAUNCH, std::string("gather launch failed: ") + hipGetErrorString(err));
+    return PRISMA_OK;
+}
+
+extern "C" int prisma_compact_pending(prisma_env_t* e, const uint8_t* mask, const int32_t* obs, const int32_t* node,
+                                      int32_t* ids_out, int32_t* obs_packed, int32_t* node_packed, int32_t* count_out,
+                                      void* stream) {
+    if (!e || !mask || !ids_out || !count_out || (obs_packed && !obs))
+        return set_err(PRISMA_ERR_ARG, "null argument (mask, ids_out and count_out are required; obs with obs_packed)");
+    (void)hipSetDevice(e->device);
+    hipLaunchKernelGGL(prisma_compact_kernel, dim3(1), dim3(kCompactThreads), 0, (hipStream_t)stream, mask, obs, node,
+                       e->R, e->lay.W, ids_out, obs_packed, node_packed, count_out);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return set_err(PRISMA_ERR_LAUNCH, std::string("compact launch failed: ") + hipGetErrorString(err));
+    return PRISMA_OK;
+}
+
+extern "C" int prisma_expand_actions(prisma_env_t* e, const int32_t* ids, const int32_t* count,
+                                     const int32_t* packed_actions, int32_t fill, int32_t* actions_out, void* stream) {
+    if (!e || !ids || !count || !packed_actions || !actions_out) return set_err(PRISMA_ERR_ARG, "null argument");
+    (void)hipSetDevice(e->device);
+    hipLaunchKernelGGL(prisma_expand_kernel, dim3(1), dim3(kCompactThreads), 0, (hipStream_t)stream, ids, count,
+                       packed_actions, e->R, fill, actions_out);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return set_err(PRISMA_ERR_LAUNCH, std::string("expand launch failed: ") + hipGetErrorString(err));
     return PRISMA_OK;
 }
 

@@ -18,7 +18,7 @@ from .topology import Topology
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprisma_amd.so")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 PRISMA_POLICY_TABLE = 1
 PRISMA_POLICY_DQN_BUFFER = 2
 PRISMA_ENGINE_AUTO, PRISMA_ENGINE_REGISTER, PRISMA_ENGINE_MEMORY = 0, 1, 2
@@ -75,6 +75,7 @@ EXPORTS = [
     "prisma_abi_version", "prisma_last_error", "prisma_build_id", "prisma_create", "prisma_reset", "prisma_step", "prisma_run",
     "prisma_read_counters", "prisma_counters_device", "prisma_log_view", "prisma_copy_log",
     "prisma_copy_counters", "prisma_gather_records", "prisma_state_bytes", "prisma_plan", "prisma_destroy",
+    "prisma_compact_pending", "prisma_expand_actions",
 ]
 
 _lib = None
@@ -122,6 +123,11 @@ def load_library(path: str = None):
     L.prisma_copy_counters.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.prisma_gather_records.restype = C.c_int
     L.prisma_gather_records.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p]
+    L.prisma_compact_pending.restype = C.c_int
+    L.prisma_compact_pending.argtypes = [C.c_void_p] + [C.c_void_p] * 7 + [C.c_void_p]
+    L.prisma_expand_actions.restype = C.c_int
+    L.prisma_expand_actions.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
+                                        C.c_void_p]
     L.prisma_state_bytes.restype = C.c_int
     L.prisma_state_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.prisma_plan.restype = C.c_int
@@ -259,6 +265,34 @@ class PrismaEngine:
         _check(_lib.prisma_step(self.h, a or None, self.obs.data_ptr(), self.mask.data_ptr(), self.node.data_ptr(),
                                 _stream_handle(stream)))
         return self.obs, self.mask, self.node
+
+    def compact_pending(self, stream=None):
+        """The pending replicas of the last step() as a dense batch (prisma_compact_pending):
+        (ids int32 [n], obs int32 [n, W], node int32 [n]) for a policy that evaluates only the
+        notified replicas (ns3env.py:417-423). One host read of the count."""
+        import torch
+        if not hasattr(self, "_cids"):
+            self._cids = torch.empty(self.R, dtype=torch.int32, device=self.torch_device)
+            self._cobs = torch.empty((self.R, self.W), dtype=torch.int32, device=self.torch_device)
+            self._cnode = torch.empty(self.R, dtype=torch.int32, device=self.torch_device)
+            self._ccount = torch.zeros(1, dtype=torch.int32, device=self.torch_device)
+        _check(_lib.prisma_compact_pending(self.h, self.mask.data_ptr(), self.obs.data_ptr(), self.node.data_ptr(),
+                                           self._cids.data_ptr(), self._cobs.data_ptr(), self._cnode.data_ptr(),
+                                           self._ccount.data_ptr(), _stream_handle(stream)))
+        n = int(self._ccount.item())
+        return self._cids[:n], self._cobs[:n], self._cnode[:n]
+
+    def expand_actions(self, ids, packed_actions, fill: int = 0, stream=None):
+        """Actions of a compacted batch back to one per replica (prisma_expand_actions), ready
+        for step(); replicas without a pending decision get `fill`."""
+        import torch
+        out = torch.empty(self.R, dtype=torch.int32, device=self.torch_device)
+        cnt = torch.tensor([int(ids.numel())], dtype=torch.int32, device=self.torch_device)
+        ids_c = ids.to(torch.int32).contiguous()
+        act = packed_actions.to(torch.int32).contiguous()
+        _check(_lib.prisma_expand_actions(self.h, ids_c.data_ptr(), cnt.data_ptr(), act.data_ptr(), int(fill),
+                                          out.data_ptr(), _stream_handle(stream)))
+        return out
 
     def run(self, policy, max_hops: int, stream=None):
         """Fused in-kernel policy: every replica executes up to max_hops hops.

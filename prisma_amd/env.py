@@ -171,7 +171,7 @@ class VecRoutingEnv:
                  [("obs", (W,), torch.int32), ("action", (), torch.int32), ("reward", (), torch.float64),
                   ("next_obs", (W,), torch.int32), ("done", (), torch.bool), ("node", (), torch.int32),
                   ("replica", (), torch.int32), ("uid", (), torch.int64), ("hop", (), torch.bool),
-                  ("t_ns", (), torch.int64)]}
+                  ("t_ns", (), torch.int64), ("episode", (), torch.int64)]}
         if total == 0:
             return empty
         rep = torch.repeat_interleave(torch.arange(self.R, device=self.device), n)
@@ -211,6 +211,9 @@ class VecRoutingEnv:
                               torch.zeros(int(dr.sum()), dtype=torch.bool, device=self.device)]),
             # when the transition completed: the next notification (hop) or the drop (loss)
             "t_ns": torch.cat([cur_f["t_ns"][hp], cur_f["t_ns"][dr]]).to(torch.int64),
+            # the episode (mod 256) it completed in: the trainer does not queue an old episode's
+            # hop transitions into the next one
+            "episode": torch.cat([cur_f["episode"][hp], cur_f["episode"][dr]]).to(torch.int64),
         }
         return out
 

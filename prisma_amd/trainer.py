@@ -58,7 +58,13 @@ argument_parser.py:41):
     (``_get_upcoming_events_real``, forwarder.py:477-490: the first queued match; lost echoes
     lose it); the NN's last segment (``nn_max_seg_index``) sets the target copy to temp if the
     NN index is u's sync counter - 1, else to upcoming (forwarder.py:251-263).
-  - signalingSim=0 (the reference's default: the agents model the delays): the transition is
+  - signalingSim=0 (the reference's default: the agents model the delays). RECONSTRUCTION OF
+    INTENT, parity unpinned: in the reference this path cannot run. Trainer.run calls
+    self._get_upcoming_events, which only Forwarder defines; Trainer._sync_all uses
+    self._push_upcoming_event and self.big_signaling_delay, which Trainer lacks; Forwarder calls
+    self._compute_sync_step, which only Trainer defines (each an AttributeError), and
+    trainer.py:106 reads the class attribute Agent.sync_step (-1), not the per-node value
+    computed from it. What follows is the behaviour those lines evidently intend: the transition is
     queued at u for ``now + small_signaling_delay(v)`` with the packet size
     64 + 8 + 8 (deg(v) + 1) bytes (forwarder.py:101-103, 380-391), and every sync of u queues,
     per neighbour, the arrival of that neighbour's NN at ``now + big_signaling_delay(u)``
@@ -254,7 +260,8 @@ class QRoutingTrainer:
                  signaling_type: str = "ideal", nn_max_seg_index: Optional[int] = None,
                  big_signaling_size: int = 512, packet_size: int = 512, pending_cap: int = 1 << 20,
                  n_replicas: int = 1, signaling_sim: int = 1, sync_step: float = 1.0, sync_ratio: float = 0.1,
-                 link_cap: int = 500000, link_delay_ms: float = 1.0, prioritized_replay: bool = False):
+                 link_cap: int = 500000, link_delay_ms: float = 1.0, prioritized_replay: bool = False,
+                 max_snapshots: int = 32):
         if signaling_type not in ("ideal", "NN", "target"):
             raise ValueError("signaling_type must be 'ideal', 'NN' or 'target'")
         self.topo = topo
@@ -319,8 +326,17 @@ class QRoutingTrainer:
         self.clock = np.zeros(self.R)                # Agent.curr_time per simulation (s)
         self.episode = np.zeros(self.R, dtype=np.int64)
         self.sync_counter = np.full((self.R, N), -1, dtype=np.int64)
-        self.snapshots = {0: self._snapshot()}       # version -> stacked online weights
+        # A copy is a version number; a version maps to one stored generation of the stacked online
+        # weights. The weights only change in place (train_step's Adam, a caller's edits), so syncs
+        # between two changes share one stored generation (keyed on the parameters' in-place
+        # version counters). Replica clocks drift apart, so the live versions grow towards O(R);
+        # max_snapshots caps the stored generations: at the cap a sync takes the newest stored
+        # generation instead of a new one (older weights by at most the syncs since it was taken).
+        self.max_snapshots = int(max_snapshots)
+        self._gen_w = {}                             # generation key -> stacked weights
+        self._snap_gen = {}                          # version -> generation key
         self.version = 0
+        self._snap_gen[0] = self._capture()
         self.tgt_ver = np.zeros((self.R, N, D), dtype=np.int64)      # per (replica, node, action) copy
         self.up_ver = np.zeros((self.R, N, D), dtype=np.int64)
         self.tmp_ver = np.zeros((self.R, N, D), dtype=np.int64)
@@ -351,7 +367,7 @@ class QRoutingTrainer:
     def q_target(self):
         """The networks the "ideal" targets of replica 0 read (the last sync's snapshot)."""
         net = copy.deepcopy(self._eval)
-        net.load_state_dict(self.snapshots[int(self.tgt_ver[0].max())])
+        net.load_state_dict(self.weights_of(int(self.tgt_ver[0].max())))
         return net
 
     # -- acting ---------------------------------------------------------------
@@ -389,9 +405,12 @@ class QRoutingTrainer:
         self.check_sync()
 
     def advance_clock(self, now_ns, episode=None):
-        t = np.asarray(now_ns.cpu() if torch.is_tensor(now_ns) else now_ns, dtype=np.float64) / 1e9
+        t = np.asarray(now_ns.cpu() if torch.is_tensor(now_ns) else now_ns, dtype=np.float64).reshape(-1) / 1e9
+        if t.shape != (self.R,):
+            raise ValueError(f"the env reports {t.size} replica clocks but the trainer was built with "
+                             f"n_replicas={self.R}: pass QRoutingTrainer(..., n_replicas=env.R)")
         if episode is not None:
-            ep = np.asarray(episode.cpu() if torch.is_tensor(episode) else episode, dtype=np.int64)
+            ep = np.asarray(episode.cpu() if torch.is_tensor(episode) else episode, dtype=np.int64).reshape(-1)
             new = ep != self.episode
             if new.any():
                 self.new_episode(np.nonzero(new)[0])
@@ -422,6 +441,14 @@ class QRoutingTrainer:
         hop = tr["hop"].to(self.device)
         self._add({k: t[~hop.to(t.device)] for k, t in tr.items()})
         h = {k: t[hop.to(t.device)].to(self.device) for k, t in tr.items()}
+        if "episode" in h and h["node"].numel():
+            # a hop transition completed in an episode its replica has already left (reported in the
+            # step that crossed the episode end): Agent.reset drops the upcoming events
+            # (agent.py:141-145), so it is not queued into the new episode
+            cur = torch.from_numpy(self.episode % 256).to(self.device)[h["replica"].long()]
+            fresh = (h["episode"].long() % 256) == cur
+            if not bool(fresh.all()):
+                h = {k: t[fresh] for k, t in h.items()}
         n = h["node"].numel()
         if n == 0:
             return
@@ -575,8 +602,9 @@ class QRoutingTrainer:
             due = (self.clock[:, None] > (self.sync_counter + 1) * self.sync_step[None, :]) & deg[None, :]
         if not due.any():
             return
+        self._gc()
         self.version += 1
-        self.snapshots[self.version] = self._snapshot()
+        self._snap_gen[self.version] = self._capture()
         r_idx, u_idx = np.nonzero(due)
         self.tmp_ver[r_idx, u_idx] = self.up_ver[r_idx, u_idx]        # sync_neighbor_upcoming_target_q_network
         self.up_ver[r_idx, u_idx] = self.version
@@ -623,11 +651,15 @@ class QRoutingTrainer:
         """r + gamma * (1 - done) * min over the next node's filtered actions of node u's copy
         of that neighbour (per replica: the copy the replica's syncs and signalling gave u)."""
         rep = torch.zeros_like(node) if replica is None else replica.long()
-        ver = torch.from_numpy(self.tgt_ver).to(node.device)[rep, node, action]
+        ver = self.tgt_ver[rep.cpu().numpy(), node.cpu().numpy(), action.cpu().numpy()]
+        gens = {}
+        for k in np.unique(ver).tolist():            # one forward pass per stored generation
+            gens.setdefault(self._snap_gen[int(k)], []).append(k)
+        gen_of = torch.from_numpy(ver).to(node.device)
         out = torch.empty_like(reward)
-        for k in torch.unique(ver).tolist():
-            sel = ver == k
-            self._eval.load_state_dict(self.snapshots[int(k)])
+        for g, vs in gens.items():
+            sel = torch.isin(gen_of, torch.tensor(vs, dtype=gen_of.dtype, device=node.device))
+            self._eval.load_state_dict(self._gen_w[g])
             out[sel] = self._bootstrap(self._eval, node[sel], action[sel], reward[sel], next_obs[sel], done[sel])
         return out
 
@@ -684,18 +716,51 @@ class QRoutingTrainer:
     def _snapshot(self) -> dict:
         return {k: t.detach().clone() for k, t in self.q.state_dict().items()}
 
+    def _weights_key(self):
+        return tuple(int(p._version) for p in self.params)
+
+    def _capture(self):
+        """The generation key of the current online weights, stored if new (newest stored one at
+        the max_snapshots cap)."""
+        key = self._weights_key()
+        if key not in self._gen_w:
+            if len(self._gen_w) >= self.max_snapshots:
+                return self._snap_gen[max(self._snap_gen)]
+            self._gen_w[key] = self._snapshot()
+        return key
+
+    def weights_of(self, version: int) -> dict:
+        """The stacked online weights copy `version` refers to."""
+        return self._gen_w[self._snap_gen[int(version)]]
+
+    @property
+    def snapshots(self) -> dict:
+        """Stored weight generations (bounded by max_snapshots)."""
+        return self._gen_w
+
     def _gc(self):
         live = set(np.unique(np.concatenate([self.tgt_ver.ravel(), self.up_ver.ravel(), self.tmp_ver.ravel()])).tolist())
         live.add(self.version)
-        for k in [k for k in self.snapshots if k not in live]:
-            del self.snapshots[k]
+        for k in [k for k in self._snap_gen if k not in live]:
+            del self._snap_gen[k]
+        used = set(self._snap_gen.values())
+        for g in [g for g in self._gen_w if g not in used]:
+            del self._gen_w[g]
 
 
-def train(env, trainer: QRoutingTrainer, steps: int, train_every: int = 1):
+def train(env, trainer: QRoutingTrainer, steps: int, train_every: int = 1, sync_every: Optional[int] = None):
     """Drive a VecRoutingEnv (external-action mode) with the trainer's epsilon-greedy
     policy: each step applies one action per replica, hands the step's notifications and
     completed transitions to the trainer (on_step: clocks, buffers, signalling, syncs), and
-    trains every ``train_every`` steps; returns per-step mean losses."""
+    trains every ``train_every`` steps; returns per-step mean losses.
+
+    ``sync_every`` (syncs every k env steps) is gone: syncs follow each replica's simulated
+    clock and ``QRoutingTrainer(sync_step=...)`` (trainer.py:101-112). Passing it warns and
+    is otherwise ignored."""
+    if sync_every is not None:
+        import warnings
+        warnings.warn("train(sync_every=...) is ignored: syncs follow the replicas' simulated clocks; set "
+                      "QRoutingTrainer(sync_step=seconds) instead", DeprecationWarning, stacklevel=2)
     obs, info = env.reset()
     trainer.advance_clock(info["now_ns"], info.get("episode"))
     losses = []

@@ -32,10 +32,29 @@ def test_library_loads_and_exports_every_symbol():
     lib = engine.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.prisma_abi_version() == engine.ABI_VERSION == 8
+    assert lib.prisma_abi_version() == engine.ABI_VERSION == 9
     out = subprocess.run(["nm", "-D", "--defined-only", engine.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (prisma_\w+)", out))
     assert set(declared_functions()) <= exported
+
+
+def test_integration_recipe_matches_engine_sources():
+    """INTEGRATION.md §1's hand-build recipe compiles exactly buildid.ENGINE_SOURCES with
+    buildid.HIPCC_FLAGS, and the library those translation units link to leaves no prisma_*
+    symbol undefined (one defined in a unit the recipe forgot would fail at dlopen)."""
+    from prisma_amd import buildid
+    txt = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    tu = re.search(r'^TU="([^"]+)"', txt, re.M)
+    assert tu, "INTEGRATION.md lists no TU=... translation units"
+    assert [f + ".hip" for f in tu.group(1).split()] == buildid.ENGINE_SOURCES
+    flags = re.search(r'^F="([^"]+)"', txt, re.M).group(1).split()
+    assert flags == buildid.HIPCC_FLAGS
+    if not os.path.exists(engine.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build_engine()
+    out = subprocess.run(["nm", "-D", "--undefined-only", engine.LIB_PATH], capture_output=True, text=True).stdout
+    undefined = re.findall(r"\bU (\S*prisma\S*)", out)
+    assert not undefined, undefined
 
 
 def test_errors_are_status_codes_not_exits():

@@ -17,8 +17,8 @@ import torch
 
 from parity_util import compare_steady
 from prisma_amd.config import engine_params
-from prisma_amd.engine import PrismaEngine
-from prisma_amd.topology import DATA_DIR, Topology
+from prisma_amd.engine import PRISMA_ENGINE_MEMORY, PrismaEngine
+from prisma_amd.topology import DATA_DIR, Topology, sp_next_hop_table
 
 pytestmark = [pytest.mark.gpu,
               pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")]
@@ -91,6 +91,64 @@ def test_config5_er256_dqn_buffer_steady(oracle_mod):
                          net_cpu=net, label="config 5 er256 dqn_buffer")
     eng.close()
     assert out["t_compared_s"] >= 3.0
+
+
+def test_config5_er256_dqn_buffer_episode_end(oracle_mod):
+    """Config 5 across an episode end on the memory-resident engine: simTime 6 s, auto-reset, the
+    DQN-buffer agent, compared through t = 6.5 s (episode 1 reached). The memory engine keeps
+    32-bit link leaf keys (time = now + (lo - lo32(now)), prisma_engine_mem.hip), so this run
+    takes them past lo32(now) wrapping at 2^32 ns = 4.295 s, then through Simulator::Stop
+    (/root/reference/prisma/ns3/sim.cc:703-716) and the reset into episode 1."""
+    topo = Topology.example("er256")
+    net, w = _buffer_net(topo, seed=5)
+    params = engine_params(topo, sim_time_s=6.0, ping_as_obs=1, auto_reset=1, seed=100, replica_base=8190,
+                           log_capacity=65536)
+    eng = PrismaEngine(topo, params, 1)
+    assert eng.engine_kind == PRISMA_ENGINE_MEMORY
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("mlp", w), t_target_s=6.5, hops_per_launch=16384,
+                         min_episode=1, net_cpu=net, label="config 5 er256 dqn_buffer 6-s episodes")
+    eng.close()
+    assert out["t_compared_s"] >= 6.5 and min(out["episodes"]) >= 1 and out["max_clock_s"] > 4.3
+
+
+@pytest.mark.parametrize("name,policy", [("abilene", "table"), ("abilene", "mlp"), ("geant", "table"),
+                                         ("geant", "mlp")])
+def test_mem_engine_forced_long_run(oracle_mod, name, policy):
+    """The register engine's workloads forced onto the memory-resident engine for 15 s of
+    simulated time (clock past 2^32 ns, FIFOs at their limit, ring and uid wrap)."""
+    topo = Topology.example(name, 0, 1.5)
+    if policy == "table":
+        net, pol = None, ("table", sp_next_hop_table(topo))
+    else:
+        net, w = _buffer_net(topo, seed=13)
+        pol = ("mlp", w)
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=1, seed=31, replica_base=600, log_capacity=65536,
+                           engine=PRISMA_ENGINE_MEMORY)
+    eng = PrismaEngine(topo, params, 2)
+    assert eng.engine_kind == PRISMA_ENGINE_MEMORY
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, pol, t_target_s=15.0, hops_per_launch=16384,
+                         net_cpu=net, label=f"memory engine {name} {policy}")
+    eng.close()
+    assert out["t_compared_s"] >= 15.0
+
+
+def test_config5_er256_big_signaling_long_run(oracle_mod):
+    """Config 5's graph with --train, "NN" echoes and big signalling (2 006 generators) on the
+    memory-resident engine past 2^32 ns: compared through t = 4.6 s."""
+    topo = Topology.example("er256")
+    table = np.load(f"{DATA_DIR}/er256/sp_next_hop_table.npy")
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=1, train=1, signaling_type="NN", big_signaling=1,
+                           big_signaling_bytes=35328, sync_step_s=0.5, seed=11, replica_base=77,
+                           log_capacity=65536)
+    eng = PrismaEngine(topo, params, 1)
+    assert eng.engine_kind == PRISMA_ENGINE_MEMORY
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("table", table), t_target_s=4.6, hops_per_launch=16384,
+                         label="config 5 er256 big signalling")
+    eng.close()
+    assert out["t_compared_s"] >= 4.6
 
 
 def test_config5_er256_sp_table_steady(oracle_mod):

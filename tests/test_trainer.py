@@ -1,5 +1,6 @@
 """Replay buffers and the Q-routing trainer (prisma_amd/trainer.py) against the
 reference's own ReplayBuffer (fixture) and restatements of learner.py / trainer.py math, on CPU."""
+import copy
 import json
 import os
 
@@ -455,10 +456,12 @@ class _RefAgents:
             self.counter[r, u] += 1
 
 
-def test_signaling_sim0_nn_queues_follow_the_reference():
-    """signalingSim=0 with "NN": hop transitions reach u's buffer small_signaling_delay(v) after
-    their notification, every sync queues the neighbours' NNs for big_signaling_delay(u), and the
-    target copies follow, per replica, against the literal restatement above."""
+def test_signaling_sim0_nn_queues_follow_the_reconstruction():
+    """signalingSim=0 with "NN" (a reconstruction of the reference's intent: its own path raises
+    AttributeError, trainer.py module docstring): hop transitions reach u's buffer
+    small_signaling_delay(v) after their notification, every sync queues the neighbours' NNs for
+    big_signaling_delay(u), and the target copies follow, per replica, against the literal
+    restatement above."""
     topo = Topology.example("abilene")
     R = 3
     tr = QRoutingTrainer(topo, "buffer", seed=2, device="cpu", signaling_type="NN", signaling_sim=0,
@@ -509,8 +512,10 @@ def test_signaling_sim0_nn_queues_follow_the_reference():
     assert tr.big_pkts > 0 and tr.small_pkts > 0 and bool((tr.tgt_ver > 0).any())
 
 
-def test_compute_sync_step_matches_trainer_formula():
-    """trainer.py:114-134: nn_size / (sum(TM) * ratio - pkts_per_s * small_signaling_pkt_size)."""
+def test_compute_sync_step_restates_trainer_formula():
+    """trainer.py:114-134's formula, nn_size / (sum(TM) * ratio - pkts_per_s * small_signaling_pkt_size)
+    (parity unpinned: the reference never reaches it -- Forwarder calls _compute_sync_step, which
+    only Trainer defines, and trainer.py:106 syncs on Agent.sync_step = -1)."""
     topo = Topology.example("abilene")
     tr = QRoutingTrainer(topo, "buffer", seed=0, device="cpu", signaling_type="NN", sync_step=-1, sync_ratio=0.1)
     from prisma_amd.trainer import convert_bps_to_data_rate
@@ -541,3 +546,72 @@ def test_echo_releases_only_the_first_queued_match_and_new_episode_drops_the_que
     tr.advance_clock(torch.tensor([5_000_000, 5_000_000]), torch.tensor([0, 1]))  # replica 1: next episode
     assert tr._pend_key.numel() == 1 and int(tr._pend["replica"][0]) == 0
     assert tr.sync_counter[1].max() == -1
+
+
+def test_snapshot_generations_stay_bounded_with_drifting_clocks():
+    """Thousands of replicas whose clocks drift apart sync at different steps: the stored weight
+    generations stay within max_snapshots, syncs between two optimizer steps share one
+    generation, and the targets still come from each copy's weights."""
+    topo = Topology.example("abilene")
+    R = 2048
+    tr = QRoutingTrainer(topo, "buffer", seed=3, device="cpu", signaling_type="NN", n_replicas=R, sync_step=0.01,
+                         batch_size=4, max_snapshots=8)
+    rng = np.random.default_rng(5)
+    clock = np.zeros(R)
+    speed = rng.random(R) * 0.004
+    g = torch.Generator().manual_seed(1)
+    for step in range(60):
+        clock += speed
+        tr.advance_clock(torch.from_numpy((clock * 1e9).astype(np.int64)))
+        tr.check_sync()
+        if step % 3 == 0:                                           # an optimizer step now and then
+            with torch.no_grad():
+                for p in tr.q.parameters():
+                    p.add_(1e-3 * torch.randn(p.shape, generator=g))
+        assert len(tr.snapshots) <= 8, (step, len(tr.snapshots))
+    assert len(set(tr.tgt_ver.ravel().tolist()) | set(tr.up_ver.ravel().tolist())) > 8   # many versions...
+    # ...each resolving to stored weights, and targets() runs one pass per stored generation
+    B = 64
+    node = torch.from_numpy(rng.integers(0, 11, B))
+    action = torch.tensor([int(rng.integers(0, topo.degrees[u])) for u in node.tolist()])
+    nobs = torch.from_numpy(rng.integers(0, 16000, (B, topo.obs_width)).astype(np.int32))
+    nobs[:, 0] = torch.from_numpy(rng.integers(0, 11, B).astype(np.int32))
+    rep = torch.from_numpy(rng.integers(0, R, B))
+    tr.tgt_ver[:] = tr.up_ver
+    got = tr.targets(node, action, torch.zeros(B), nobs, torch.zeros(B, dtype=torch.bool), rep)
+    for j in range(0, B, 8):
+        net = copy.deepcopy(tr._eval)
+        net.load_state_dict(tr.weights_of(int(tr.tgt_ver[rep[j], node[j], action[j]])))
+        want = tr._bootstrap(net, node[j:j + 1], action[j:j + 1], torch.zeros(1), nobs[j:j + 1],
+                             torch.zeros(1, dtype=torch.bool))
+        assert torch.allclose(got[j:j + 1], want, rtol=1e-6, atol=1e-6), (got[j], want)
+
+
+def test_trainer_replica_count_must_match_the_env():
+    topo = Topology.example("abilene")
+    tr = QRoutingTrainer(topo, "buffer", seed=0, device="cpu", n_replicas=4)
+    with pytest.raises(ValueError, match="n_replicas=4"):
+        tr.advance_clock(torch.zeros(8, dtype=torch.int64))
+
+
+def test_old_episode_hop_transitions_are_not_queued_and_sync_every_warns():
+    """A step that crosses a replica's episode end reports its last old-episode transitions:
+    they are not queued into the new episode (agent.py:141-145 drops the upcoming events)."""
+    topo = Topology.example("abilene")
+    tr = QRoutingTrainer(topo, "buffer", seed=6, device="cpu", signaling_type="NN", batch_size=4, n_replicas=2)
+    obs = torch.zeros((2, topo.obs_width), dtype=torch.int32)
+    b = {"node": torch.tensor([3, 3], dtype=torch.int32), "obs": obs, "next_obs": obs,
+         "action": torch.tensor([0, 0], dtype=torch.int32), "reward": torch.zeros(2, dtype=torch.float64),
+         "done": torch.zeros(2, dtype=torch.bool), "replica": torch.tensor([0, 1], dtype=torch.int32),
+         "uid": torch.tensor([5, 6]), "hop": torch.ones(2, dtype=torch.bool),
+         "t_ns": torch.tensor([1_000_000, 1_000_000]), "episode": torch.tensor([0, 0])}
+    tr.on_step(torch.zeros((2, topo.obs_width), dtype=torch.int32),
+               {"transitions": b, "now_ns": torch.tensor([2_000_000, 3_000]), "episode": torch.tensor([0, 1])})
+    assert tr._pend_key.numel() == 1 and int(tr._pend["replica"][0]) == 0
+    from prisma_amd.trainer import train
+
+    class _Env:
+        def reset(self):
+            raise RuntimeError("reached")
+    with pytest.warns(DeprecationWarning, match="sync_step"), pytest.raises(RuntimeError, match="reached"):
+        train(_Env(), tr, 1, sync_every=5)
