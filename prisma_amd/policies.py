@@ -143,12 +143,19 @@ class StackedQNet(torch.nn.Module):
         if self.kind != "routing":
             raise ValueError("only the DQ-routing model has a state-independent argmin table")
         dev = self.W1.device
-        on = torch.from_numpy(self.topo_overlay_nodes).to(dev)
+        # the (node, destination) grid is built once per device: a host-to-device copy per call
+        # (from pageable memory, non_blocking=False) synchronises the stream, so every policy
+        # refresh would wait for the engine launch before it and leave the GPU idle meanwhile
+        key = str(dev)
+        if getattr(self, "_grid_dev", None) != key:
+            on = torch.from_numpy(self.topo_overlay_nodes).to(dev)
+            no = on.numel()
+            obs = torch.zeros((no * no, 1 + self.D), dtype=torch.int32, device=dev)
+            obs[:, 0] = torch.arange(no, device=dev).repeat(no).to(torch.int32)
+            self._grid = (on, on.repeat_interleave(no), obs)
+            self._grid_dev = key
+        on, node, obs = self._grid
         no = on.numel()
-        node = on.repeat_interleave(no)
-        dsti = torch.arange(no, device=dev).repeat(no)
-        obs = torch.zeros((no * no, 1 + self.D), dtype=torch.int32, device=dev)
-        obs[:, 0] = dsti.to(torch.int32)
         a = self.act(obs, node).view(no, no)
         a.fill_diagonal_(0)                                   # at destination: action 0 (forwarder.py:149)
         table = torch.zeros((self.N, self.N), dtype=torch.uint8, device=dev)

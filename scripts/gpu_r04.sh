@@ -12,7 +12,11 @@ grep -E "steady\]" gpurun_out/steady_$TAG.log
 timeout -k 10 700 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests \
     --ignore tests/test_gpu_steady_state.py > gpurun_out/tests_$TAG.log 2>&1 || { tail -30 gpurun_out/tests_$TAG.log; exit 1; }
 tail -2 gpurun_out/tests_$TAG.log
-[ "$3" = tests ] && exit 0
+if [ "$3" = tests ]; then
+  timeout -k 10 300 python scripts/timing.py run --topology er256 --replicas 1024 --hops 8192 --policy dqn_buffer --warm 13 > gpurun_out/timing_er256_$TAG.txt 2>&1 || { tail -20 gpurun_out/timing_er256_$TAG.txt; exit 1; }
+  cat gpurun_out/timing_er256_$TAG.txt
+  exit 0
+fi
 bash scripts/configs.sh > gpurun_out/configs_$TAG.log 2>&1 || { tail -20 gpurun_out/configs_$TAG.log; exit 1; }
 tail -14 gpurun_out/configs_$TAG.log
 cp gpurun_out/configs.jsonl gpurun_out/configs_$TAG.jsonl
