@@ -223,8 +223,19 @@ struct BigSig {
 enum : uint32_t {
     LR_P0 = 0, LR_P1, LR_P2, LR_QB, LR_CPT, LR_CPS, LR_WHT, LR_WHS,
     LR_PMLO, LR_PMMLO, LR_PMMHI, LR_PMWIN, LR_PAVLO, LR_PAVHI, LR_ODLO, LR_ODHI,
-    LR_WT = 16,                  // wire slots: arrival time [WCAP], seq [WCAP], packet entry [WCAP]
+    LR_WT = 16,                  // wire slots: arrival time [WCAP], seq [WCAP], packet entry [WCAP],
+                                 // then the entry's three aux words [WCAP] each (kMemAux)
 };
-constexpr uint32_t kMemMaxWire = 16u;
+// The memory-resident engine's FIFO slots are 16 B {entry, aux0, aux1, aux2} and its wire
+// slots carry the aux words too: a forwarded data packet holds its previous decision's time
+// (low 32 bits), uid and record word 6 (deciding node | destination << 8 | start second <<
+// 16), so its next arrival reads them from the link record instead of the decision log
+// (one dependent HBM round trip less per data arrival).
+constexpr uint32_t kMemAux = 3u;
+constexpr uint32_t kMemMaxWire = 8u;             // LR_WT + (3 + kMemAux) * WCAP <= 64 words
+// Event-tree kind byte of a link leaf (LDS): kind | hint << 2, where the hint classifies the
+// packet at the wire head of a link whose next event is its arrival, so the arrival handler can
+// issue what it will need together with the link record (prefetch classes, engine_core.h)
+constexpr uint32_t kHintNone = 0u, kHintDecide = 1u, kHintDest = 2u, kHintPing = 3u;
 
 }  // namespace prisma
