@@ -405,8 +405,23 @@ __device__ __forceinline__ void ring_put(const Sim& S, uint32_t i, uint32_t e) {
 }
 
 // memory-resident engine: 16-B FIFO slots {entry, aux0, aux1, aux2} (engine_layout.h kMemAux)
+#ifndef PRISMA_RING4_LANES
+#define PRISMA_RING4_LANES 0
+#endif
+// memory-resident engine: which of a decision's weights go out with the arrival's observation
+// gather (A/B): 3 layer 1 (layers 2-4 when the decision starts), 1 layers 1-2,
+// 0 none (all at the decision)
+#ifndef PRISMA_MEM_W_EARLY
+#define PRISMA_MEM_W_EARLY 0
+#endif
 __device__ __forceinline__ void ring_put4(const Sim& S, uint32_t i, uint4 e) {
-    ((uint4*)S.ring)[i] = e;
+    if (PRISMA_RING4_LANES) {                    // (A/B variant) lanes 0-3 store one word each
+        const uint32_t j = (uint32_t)S.lane;
+        const uint32_t w = j == 0 ? e.x : (j == 1 ? e.y : (j == 2 ? e.z : e.w));
+        if (j < 4) ((uint32_t*)S.ring)[4u * i + j] = w;
+    } else {
+        ((uint4*)S.ring)[i] = e;
+    }
 }
 __device__ __forceinline__ uint4 ring_get4(const Sim& S, uint32_t i) {
     const uint4 v = ((const uint4*)S.ring)[i];
@@ -500,7 +515,8 @@ struct LinkV {
     uint32_t wh_t, wh_seq;       // wire-head arrival time (low 32 bits), seq
     uint32_t rec;                // memory-resident engine: the link's record, lane j = word j
     uint32_t wmod;               // memory-resident: wire slot written since the load (~0: none)
-    uint32_t hint;               // memory-resident: prefetch class of the wire-head packet
+    uint32_t aux;                // memory-resident: the link's wire aux block, lane 4i + m = aux word m
+                                 // of slot i (loaded by arrivals; written for the slot wmod)
 };
 
 template <int FS, int LS>
@@ -655,10 +671,12 @@ __device__ __forceinline__ void wire_set(const Sim& S, LinkV& k, uint32_t l, uin
         v = j == LR_WT + i ? t : v;
         v = j == LR_WT + W + i ? s : v;
         v = j == LR_WT + 2u * W + i ? x : v;
-        v = j == LR_WT + 3u * W + i ? ax.y : v;
-        v = j == LR_WT + 4u * W + i ? ax.z : v;
-        v = j == LR_WT + 5u * W + i ? ax.w : v;
         k.rec = v;
+        uint32_t a = k.aux;
+        a = j == 4u * i ? ax.y : a;
+        a = j == 4u * i + 1u ? ax.z : a;
+        a = j == 4u * i + 2u ? ax.w : a;
+        k.aux = a;
         k.wmod = i;
     } else {                                  // every lane stores the same value to the same address:
         S.wt[l * W + i] = t;                  // no exec-mask juggling (A/B +1 % against lane 0 only)
@@ -680,21 +698,10 @@ __device__ __forceinline__ void wire_get(const Sim& S, const LinkV& k, uint32_t 
 __device__ __forceinline__ uint32_t wire_ent(const Sim& S, const LinkV& k, uint32_t i) {
     return rdl(k.rec, LR_WT + 2u * (uint32_t)S.lv.WCAP() + i);
 }
-// memory-resident engine: aux word m (< kMemAux) of wire slot i
+// memory-resident engine: aux word m (< kMemAux) of wire slot i (the arrival's aux block load)
 __device__ __forceinline__ uint32_t wire_aux(const Sim& S, const LinkV& k, uint32_t i, uint32_t m) {
-    return rdl(k.rec, LR_WT + (3u + m) * (uint32_t)S.lv.WCAP() + i);
+    return rdl(k.aux, 4u * i + m);
 }
-// prefetch class of packet x (aux word 2 = a relay's record word 6) at the head of link l's
-// wire (engine_layout.h kHint*): a data packet that will be decided on at the far end, a data
-// packet at its destination, a ping; anything else (echoes, big signalling) none
-__device__ __forceinline__ uint32_t ent_hint(const Sim& S, uint32_t x, uint32_t a2, uint32_t l) {
-    if (ent_is_data(x)) {
-        const uint32_t dst = ent_type(x) == T_FRESH ? f_dst(x) : ((a2 >> 8) & 255u);
-        return dst == (uint32_t)t_ldst(S, l) ? kHintDest : kHintDecide;
-    }
-    return (S.ctrl && (ent_is_echo(x) || ent_is_big(x))) ? kHintNone : kHintPing;
-}
-
 // ---- link FIFO / transmitter (point-to-point-net-device.cc:273-336, 595-666)
 __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l, LinkV& k, uint32_t ring_idx,
                                                uint32_t x, uint4 ax = uint4{}) {
@@ -719,10 +726,7 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
     const uint32_t at = lo32(H.now + tx + prop);
     const uint32_t as = H.seq++;                               // channel Receive
     wire_set(S, k, l, w, at, as, x, ax);
-    if (k.n_wire == 1) {                                       // the wire was empty: new head
-        k.wh_t = at; k.wh_seq = as;
-        if (S.mem) k.hint = ent_hint(S, x, ax.w, l);
-    }
+    if (k.n_wire == 1) { k.wh_t = at; k.wh_seq = as; }        // the wire was empty: new head
     if (k.n_wire > (uint32_t)L.WCAP()) fail(H, PRISMA_EBIT_WIRE);
 }
 
@@ -999,14 +1003,11 @@ __device__ __forceinline__ uint32_t tunnel_link(const Sim& S, uint32_t t) {
 // d at node v, then the Receive tail.  x is the arriving entry (for the
 // counters); fused: the record is written here once, with the final status
 // (table policy).
-// KP (memory-resident engine without the ctrl paths): `kp` is the chosen out-link's state,
-// fetched with the arrival (link_from_words), so the send needs no load
-template <bool KP = false, class RS>
+template <class RS>
 __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint32_t x, uint32_t dst,
                                                uint32_t start, uint32_t uid, uint32_t v, uint32_t d, int action,
                                                bool fused, double reward, int32_t prev, uint32_t obs_reg,
-                                               uint32_t echo_link, uint32_t last, uint32_t ttl,
-                                               LinkV kp = LinkV{}) {
+                                               uint32_t echo_link, uint32_t last, uint32_t ttl) {
     const LV& L = S.lv;
 #if PRISMA_TIMING
     S.tlast = TM_NOW();
@@ -1026,9 +1027,7 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
         const uint32_t fwd = (PRISMA_ABLATE & 1) ? (T_RELAY | (dst << 2) | (start << 10) | (src << 24)) : r_make(d, src);
         // memory-resident: the decision's time, uid and record word 6 ride with the packet
         const uint4 ax = make_uint4(0u, lo32(H.now), uid, v | (dst << 8) | (start << 16));
-        int sent;
-        if constexpr (KP) sent = link_send_k(S, R, H, l, fwd, kp, ax);
-        else sent = RS::kMem ? link_send(S, R, H, l, fwd, ax) : link_send(S, R, H, l, fwd);
+        const int sent = RS::kMem ? link_send(S, R, H, l, fwd, ax) : link_send(S, R, H, l, fwd);
         if (sent) {                                               // lastHop = v, previous decision = d
             status = PRISMA_ST_ENQUEUED;
         } else {
@@ -1290,8 +1289,8 @@ struct MlpPre1 {
     float b1v;
     float w1v;                   // the one-hot row element, when the destination was known (has_w1)
     bool has_w1;
-    // (mlp_action PRE == 2: the memory-resident arrival's kHintDecide prefetch, issued with the
-    // link record) the buffer-branch chunks 4-7 (degrees 17-32) too
+    // (mlp_action PRE == 2, the memory-resident engine) the buffer-branch chunks 4-7 (degrees
+    // 17-32) too
     float4 wx[4];
 };
 
@@ -1341,16 +1340,32 @@ __device__ __forceinline__ void mlp_preload_node(MlpPre1& M, const Sim& S, uint3
     M.b1v = (lane < 32) ? RP1[128 * ((D + 3) / 4) + 32 + j32] : RP1[128 * ((D + 3) / 4) + j32];
 }
 
+// layer 1 of a decision at node v (buffer branch chunks 0-7 and biases) for mlp_action PRE 3
+__device__ __forceinline__ void mlp_preload_l1(MlpPre1& M, const Sim& S, uint32_t v) {
+    const int lane = S.lane;
+    v = rfl(v);
+    const int D = S.lv.max_deg();
+    const float* __restrict__ RP1 = S.mlp_rp + (size_t)v * mlp_rp_node_floats(D);
+    const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
+    const int j32 = lane & 31, nck = (deg + 3) >> 2;
+    const float4* __restrict__ Wb4 = (const float4*)RP1;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) M.wb[c] = Wb4[(c < nck ? c : 0) * 32 + j32];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) M.wx[c] = Wb4[((c + 4 < nck) ? c + 4 : 0) * 32 + j32];
+    M.b1v = (lane < 32) ? RP1[128 * ((D + 3) / 4) + 32 + j32] : RP1[128 * ((D + 3) / 4) + j32];
+}
+
 // the one-hot row element W1[v][dst][j] of lane j < 32 (models.py:258-306's one-hot branch)
 __device__ __forceinline__ float mlp_row_elem(const Sim& S, uint32_t v, uint32_t dst) {
     return S.lane < 32 ? S.mlp[((int)rfl(v) * S.lv.N() + (int)rfl(dst)) * 32 + (S.lane & 31)] : 0.0f;
 }
-// layers 1-2 of a decision at node v but the one-hot row element (the destination is not known
-// yet): issued by the memory-resident arrival together with the link record when the wire
-// head's hint says the packet will be decided on (kHintDecide).  Layers 3-4 load when the
-// decision starts (mlp_action): they are first needed a LayerNorm and two layers later, past
-// one HBM round trip, and holding them through the arrival cost spills.
-__device__ __forceinline__ void mlp_preload_all(MlpPre1& M, const Sim& S, uint32_t v) {
+// layers 1-2 of a decision at node v (buffer branch with chunks 4-7, biases, layer 2) for
+// mlp_action PRE 2; the memory-resident engine issues them with the arrival's observation
+// gather as soon as the link record shows a packet to decide on (mlp_row_elem adds the one-hot
+// row element).  Layers 3-4 load when the decision starts (mlp_action): they are first needed
+// two layers later.
+__device__ __forceinline__ void mlp_preload_l12(MlpPre1& M, const Sim& S, uint32_t v) {
     const int lane = S.lane;
     v = rfl(v);
     const int D = S.lv.max_deg();
@@ -1503,7 +1518,8 @@ __device__ __forceinline__ int lane_argmin_first(float q, int n) {
 }
 
 // PRE: 0 every weight loaded here; 1 (memory-resident arrival) layers 1-2 in P1 and, when
-// P1.has_w1, the one-hot row element; 2 layers 1-2 with buffer chunks 4-7 and the row element in P1
+// P1.has_w1, the one-hot row element; 2 layers 1-2 with buffer chunks 4-7 and the row element in
+// P1; 3 layer 1 (chunks 0-7, bias, row element) in P1, layers 2-4 loaded here
 template <int B, int PRE = 0>
 __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs_reg, const MlpPre1& P1) {
     const LV& L = S.lv;
@@ -1534,15 +1550,15 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     const int nck = (deg + 3) >> 2;
     const float4* __restrict__ Wb4 = (const float4*)RP1;
     float w1v;
-    if (PRE == 2 || (PRE && P1.has_w1)) w1v = P1.w1v;
+    if (PRE >= 2 || (PRE && P1.has_w1)) w1v = P1.w1v;
     else w1v = (lane < 32) ? W1[((int)v * N + (int)dst) * 32 + j32] : 0.0f;
     // memory-resident engine: buffer-branch chunks 4-7 (degrees 17-32) are loaded here, BEFORE
     // the layer 3-4 stream: the load counter is in order, so a chunk loaded inside layer 1
     // made layer 1 wait for the whole stream (and the compiler, unable to count the loop's
     // loads, waited for everything before layer 2)
     float4 wx[4];
-    if constexpr (B == kMlpAll && PRE == 2) {
-        // (every weight in P1: used in place below)
+    if constexpr (B == kMlpAll && PRE >= 2) {
+        // (chunks 4-7 in P1: used in place below)
     } else if constexpr (B == kMlpAll) {
         // (always issued, chunk 0 again past the node's degree: no branch for the scheduler to
         // hoist the stream's loads above)
@@ -1551,10 +1567,11 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
         __builtin_amdgcn_sched_barrier(0);
     }
     MlpPre M;
-    if constexpr (B == kMlpAll) mlp_preload(M, RP, lane, D, deg, !PRE);   // PRE: layer 2 came with the arrival
+    // (PRE 1, 2: layer 2 came with the arrival)
+    if constexpr (B == kMlpAll) mlp_preload(M, RP, lane, D, deg, PRE == 0 || PRE == 3);
     float b1v;
     float4 wb[4];
-    if constexpr (PRE == 2) {
+    if constexpr (PRE >= 2) {
         b1v = P1.b1v;
     } else if constexpr (PRE) {
         b1v = P1.b1v;
@@ -1604,7 +1621,7 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
             if (c < nck) {
-                if constexpr (PRE == 2) chunk(c, c < 4 ? P1.wb[c & 3] : P1.wx[c & 3]);
+                if constexpr (PRE >= 2) chunk(c, c < 4 ? P1.wb[c & 3] : P1.wx[c & 3]);
                 else chunk(c, c < 4 ? wb[c & 3] : wx[c & 3]);
             }
         }
@@ -1630,7 +1647,7 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
         __builtin_amdgcn_wave_barrier();
         return lane_argmin_first_seq(q4, deg);
     }
-    if constexpr (PRE) h = det_elu(mlp_dense64_pre(S, P1.w2, P1.b2));
+    if constexpr (PRE == 1 || PRE == 2) h = det_elu(mlp_dense64_pre(S, P1.w2, P1.b2));
     else if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w2, M.b2));
     else h = det_elu(mlp_dense64<B>(S, RP, lane, 64));
     __builtin_amdgcn_wave_barrier();
@@ -1669,35 +1686,19 @@ __device__ __forceinline__ void wire_pop(const Sim& S, RS& R, const Hot& H, uint
     if (k.n_wire) {                                                 // next packet on the wire
         const uint32_t w = k.head & (uint32_t)(L.WCAP() - 1);
         wire_get(S, k, l, w, k.wh_t, k.wh_seq);
-        if constexpr (RS::kMem) k.hint = ent_hint(S, wire_ent(S, k, w), wire_aux(S, k, w, 2u), l);
     }
     link_put<LP_WIRE>(S, R, H, l, k);
 }
 
 struct Decision {
     uint32_t x, dst, start, uid, v, d; double reward; int32_t prev; uint32_t obs, flags, last, ttl;
+    int tab;                     // memory-resident table policy: the action, read with the observation
 };
 
-// The memory-resident arrival's prefetch (engine_layout.h kHint*): what the handler will need,
-// issued together with the link record, so an arrival waits for one HBM round trip
-struct ArrPre {
-    uint32_t o[8];               // kHintDecide: words 0-7 of the deciding node's out-links (lane a + 1
-                                 // holds out-link a; lanes past the degree hold out-link 0's)
-    uint32_t pw[5];              // ... and their ping words PMLO, PAVLO, PAVHI, ODLO, ODHI (pingAsObs)
-    uint32_t prec, pwin, ppbd;   // kHintPing: the record of the link back to the sender (lane j = word j),
-                                 // its ping window (lane i < MA) and ping-back delay slots (lane i < PBK)
-    bool out;                    // o[] / pw[] hold node D.v's out-links
-    bool mlp;                    // every weight of the decision is in the MlpPre1 (mlp_action PRE 2)
-    bool ping;                   // prec / pwin / ppbd are valid
-    bool pop;                    // the arrival's wire pop is left to the caller, after the decision
-                                 // (the link is not the decision's; the tree repair then runs after
-                                 // the weights are dead, not while they fill the registers)
-    LinkV kl;                    // ... the arrival link's state for it
-};
 // the memory-resident engine's arrival (prisma_engine_mem.hip)
 template <bool MLPK, class RS>
-__device__ __forceinline__ int on_arrive_mem(const Sim& S, RS& R, Hot& H, uint32_t l, uint32_t hint, Decision& D,
-                                             bool fused, MlpPre1& Mp, ArrPre& A);
+__device__ __forceinline__ int on_arrive_mem(const Sim& S, RS& R, Hot& H, uint32_t l, Decision& D, bool fused,
+                                             MlpPre1& Mp, bool& pre);
 
 // a control packet (or a data packet inside a tunnel) continues along the
 // underlay route to `to` (Ipv4L3Protocol::IpForward through the patched
@@ -1710,22 +1711,15 @@ __device__ __forceinline__ void ctrl_forward(const Sim& S, RS& R, Hot& H, uint32
 
 // PingBackPacketManager::receivePacket (ping-back-packet-manager.cc:120-144) on
 // tunnel lt with the one-hop delay the ping-back carries
-// (PF, memory-resident engine: tunnel lt's link record `prec` -- lane j = word j -- and its
-// window `pwin` -- lane i = slot i -- were fetched with the arrival's link record)
-template <bool PF = false, class RS>
+template <class RS>
 __device__ __forceinline__ void ping_ack(const Sim& S, RS& R, Hot& H, uint32_t lt, uint32_t rnd,
-                                         float delay, uint32_t prec = 0u, uint32_t pwin = 0u) {
+                                         float delay) {
     const LV& L = S.lv;
     // the round itself (rounds in flight are less than 2^18 behind the last one sent)
     const uint32_t last = H.ping_rounds - 1u;
     const uint32_t k = last - ((last - rnd) & kRoundMask);
     // erase round k from the unacknowledged list (first match; none if already acked)
-    PingV pv;
-    if constexpr (PF) {
-        pv.lo = rdl(prec, LR_PMLO); pv.mlo = rdl(prec, LR_PMMLO); pv.mhi = rdl(prec, LR_PMMHI); pv.win = rdl(prec, LR_PMWIN);
-    } else {
-        pv = ping_get(S, R, lt);
-    }
+    const PingV pv = ping_get(S, R, lt);
     uint32_t lo = pv.lo;
     uint64_t mask = ((uint64_t)pv.mhi << 32) | pv.mlo;
     uint32_t pw = pv.win;
@@ -1762,8 +1756,7 @@ __device__ __forceinline__ void ping_ack(const Sim& S, RS& R, Hot& H, uint32_t l
     double sum = 0.0;
     uint32_t i = wh;
     for (uint32_t j = 0; j < wn; ++j) {
-        float w = (i == slot) ? delay
-                              : __uint_as_float(PF ? rdl(pwin, i) : u_ld32((const uint32_t*)S.win + lt * MA + i));
+        float w = (i == slot) ? delay : __uint_as_float(u_ld32((const uint32_t*)S.win + lt * MA + i));
         sum += (double)w;
         i = (i + 1 == MA) ? 0 : i + 1;
     }
@@ -2350,50 +2343,34 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
         }
 #endif
         H.ev_launch++;                                   // added to the events counter at exit
-        // (memory-resident engine: a link leaf's code carries its wire head's prefetch hint in
-        // bits 30-31, engine_layout.h kHint*)
-        const uint32_t kind = RS::kMem ? ((bc >> 28) & 3u) : (bc >> 28), id = bc & 0x0fffffffu;
+        const uint32_t kind = bc >> 28, id = bc & 0x0fffffffu;
         TM_MARK(0);
         if (kind == K_ARRIVE) {
             Decision D;
             MlpPre1 Mp;                                  // (kPre) the decision's weights, fetched on arrival
-            ArrPre A;                                    // (memory-resident) the rest of the prefetch
+            bool pre = false;                            // (memory-resident) layers 1-2 already in Mp
             int need;
-            if constexpr (RS::kMem) need = on_arrive_mem<MLP>(S, R, H, id, bc >> 30, D, table_mode, Mp, A);
+            if constexpr (RS::kMem) need = on_arrive_mem<MLP>(S, R, H, id, D, table_mode, Mp, pre);
             else need = on_arrive<kPre>(S, R, H, id, D, table_mode, Mp);
             TM_MARK(1);
             if (need) {
                 if (table_mode) {
                     int a;
                     if constexpr (RS::kMem && MLP) {
-                        if (!A.mlp) {                    // (no prefetch: every weight now)
-                            mlp_preload_all(Mp, S, D.v);
+                        if (!pre) {                      // (not issued with the arrival: now)
+                            if (PRISMA_MEM_W_EARLY == 3) mlp_preload_l1(Mp, S, D.v);
+                            else mlp_preload_l12(Mp, S, D.v);
                             Mp.w1v = mlp_row_elem(S, D.v, D.dst);
                         }
-                        a = mlp_action<MB, 2>(S, D.v, D.obs, Mp);
+                        a = mlp_action<MB, PRISMA_MEM_W_EARLY == 3 ? 3 : 2>(S, D.v, D.obs, Mp);
+                    } else if constexpr (RS::kMem) {
+                        a = D.tab;                       // (on_arrive_mem read it with the observation)
                     } else {
                         a = mlp_mode ? mlp_action<MB, kPre>(S, D.v, D.obs, Mp) : table_action(S, D.v * NN + D.dst);
                     }
-                    const uint32_t echo_l = (D.flags & PEND_ECHO) ? (uint32_t)t_lrev(S, id) : kNoLink;
-                    bool sent_pre = false;
-                    if constexpr (RS::kMem) {
-                        // the chosen out-link's state came with the arrival (not in the ctrl
-                        // instances: their echo may have changed it since)
-                        const uint32_t v = rfl(D.v);
-                        const int r0 = t_ovrow(S, v), deg = t_ovrow(S, v + 1) - r0;
-                        if (!S.ctrl && A.out && a >= 0 && a < deg) {
-                            const LinkV kp = link_from_words(R, (uint32_t)(r0 + a), A.o, (uint32_t)a + 1u);
-                            apply_decision<true>(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, a, true,
-                                                 D.reward, D.prev, D.obs, echo_l, D.last, D.ttl, kp);
-                            sent_pre = true;
-                        }
-                    }
-                    if (!sent_pre)
-                        apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, a, true,
-                                       D.reward, D.prev, D.obs, echo_l, D.last, D.ttl);
-                    if constexpr (RS::kMem) {
-                        if (A.pop) wire_pop(S, R, H, id, A.kl);
-                    }
+                    apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, a, true,
+                                   D.reward, D.prev, D.obs,
+                                   (D.flags & PEND_ECHO) ? (uint32_t)t_lrev(S, id) : kNoLink, D.last, D.ttl);
                     H.hops_launch++;
                     if (H.hops_launch >= max_hops) H.stop = 1;
                     TM_MARK(2);

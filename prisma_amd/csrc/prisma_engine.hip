@@ -484,8 +484,8 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
                       std::vector<unsigned char>& topo, const std::vector<int64_t>& acctx,
                       const std::vector<int32_t>& ldst, uint32_t ring_total, const Signal& SG) {
     const int N = T->n_nodes, E = T->n_links, F = T->n_flows, Lk = E + N;
-    if (L.WCAP > (int)kMemMaxWire) return set_err(PRISMA_ERR_CONFIG, "more than 8 packets on a wire (memory-resident engine)");
-    L.lrec_words = LR_WT + (3u + kMemAux) * (uint32_t)L.WCAP <= 32u ? 32u : 64u;
+    if (L.WCAP > (int)kMemMaxWire) return set_err(PRISMA_ERR_CONFIG, "more than 16 packets on a wire (memory-resident engine)");
+    L.lrec_words = LR_WT + 3u * (uint32_t)L.WCAP <= 32u ? 32u : 64u;
     // event sources: links, flows, and the big-signalling generators' one slot (on_bsig)
     const uint32_t FG = (uint32_t)F + (SG.bs.n_gen ? 1u : 0u);
     const uint64_t n_leaf = (uint64_t)Lk + (uint64_t)FG;
@@ -541,6 +541,7 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
     L.lds_state_bytes = (uint32_t)o;
     L.g_lrec = take(4u * L.lrec_words * (uint64_t)Lk);
     L.g_keys = take(16u * (uint64_t)FG);
+    L.g_laux = take(16u * (uint64_t)L.WCAP * (uint64_t)Lk);     // 4 words per wire slot (kMemAux + pad)
     L.s_ring = take(16u * (uint64_t)ring_total);            // 16-B slots {entry, aux} (kMemAux)
     L.s_win = take(4u * (uint64_t)E * L.MA);
     L.s_pbd = take(4u * (uint64_t)E * L.PBK);

@@ -26,12 +26,13 @@ struct MemSt {
     static constexpr bool kLazy = true;          // empty-queue transmit completions elided (lazy_resolve)
     static constexpr bool kMem = true;
     uint32_t* lrec;              // [L][RW] link records (HBM)
+    uint32_t* laux;              // [L][AW] wire aux blocks (HBM, engine_layout.h kMemAux)
     uint4* fkeys;                // [F] flow leaf keys {t lo, t hi, seq, draw} (HBM)
     uint2* lkey;                 // LDS [L] link leaf keys {t lo, seq}: t = now + (t lo - lo32(now))
     uint8_t* lkind;              // LDS [L] link event kind (0: none, K_COMPLETE, K_ARRIVE)
     uint4* lv1;                  // LDS [n1] {t lo, t hi, seq, code}
     uint4* lv2;                  // LDS [n2]
-    uint32_t L, n_leaf, n1, n2, RW, WCAP;
+    uint32_t L, n_leaf, n1, n2, RW, WCAP, AW;
     // the 64-leaf block of the flow whose send event runs, loaded (one coalesced 1 KiB
     // load) by flow_draw for its draw index; flow_set re-reduces the block from it instead
     // of storing the new key and loading the block back (one HBM round trip per flow event)
@@ -41,10 +42,8 @@ struct MemSt {
 
 constexpr int64_t kInf = INT64_MAX;
 
-// code = kind << 28 | source index; a link leaf's kind byte has its prefetch hint in bits 2-3
-// (code bits 30-31)
 __device__ __forceinline__ uint32_t leaf_of(const MemSt& R, uint32_t code) {
-    return ((code >> 28) & 3u) == K_FLOW ? R.L + (code & 0x0fffffffu) : (code & 0x0fffffffu);
+    return (code >> 28) == K_FLOW ? R.L + (code & 0x0fffffffu) : (code & 0x0fffffffu);
 }
 
 // uniform (t, seq, code) minimum over the lanes (lowest (t, seq); seqs are unique
@@ -218,30 +217,19 @@ __device__ __forceinline__ LinkV link_from_rec(const MemSt& R, uint32_t l, uint3
     k.wh_t = rdl(k.rec, LR_WHT);
     k.wh_seq = rdl(k.rec, LR_WHS);
     k.wmod = ~0u;
-    k.hint = rfl((uint32_t)R.lkind[l]) >> 2;               // (LDS, read while the record loads)
+    k.aux = 0u;
     return k;
 }
 __device__ __forceinline__ LinkV link_get(const MemSt& R, uint32_t l) { return link_from_rec(R, l, rec_load(R, l)); }
-// a link's fields from words 0-7 held lane-distributed (lane `at` holds word w of the link in
-// register w: the arrival's prefetch of the deciding node's out-links); no wire slot is loaded,
-// so link_put writes back the fields and the slot a send fills only
-__device__ __forceinline__ LinkV link_from_words(const MemSt& R, uint32_t l, const uint32_t (&o)[8], uint32_t at) {
-    LinkV k;
-    const uint32_t p0 = rdl(o[LR_P0], at), p1 = rdl(o[LR_P1], at), p2 = rdl(o[LR_P2], at);
-    k.head = p0 & 0xffffu; k.txp = p0 >> 16;
-    k.tail = p1 & 0xffffu; k.n_wire = p1 >> 16;
-    k.n_queue = p2 & 0xffffu; k.busy = p2 >> 16;
-    k.qb = rdl(o[LR_QB], at);
-    k.cp_t = rdl(o[LR_CPT], at);
-    k.cp_seq = rdl(o[LR_CPS], at);
-    k.wh_t = rdl(o[LR_WHT], at);
-    k.wh_seq = rdl(o[LR_WHS], at);
-    k.rec = 0u;
-    k.wmod = ~0u;
-    k.hint = rfl((uint32_t)R.lkind[l]) >> 2;
+// an arrival's link state: the record and the wire aux block, loaded together
+__device__ __forceinline__ LinkV link_get_aux(const MemSt& R, uint32_t l) {
+    const uint32_t j = threadIdx.x;
+    const uint32_t rec = rec_load(R, l);
+    const uint32_t aux = j < R.AW ? R.laux[l * R.AW + j] : 0u;
+    LinkV k = link_from_rec(R, l, rec);
+    k.aux = aux;
     return k;
 }
-
 template <unsigned MASK = LP_ALL>                 // (the whole record is written back either way)
 __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, uint32_t l, const LinkV& k) {
     const uint32_t j = threadIdx.x;
@@ -254,11 +242,12 @@ __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, u
     w = j == LR_CPS ? k.cp_seq : w;
     w = j == LR_WHT ? k.wh_t : w;
     w = j == LR_WHS ? k.wh_seq : w;
-    // the fields, and the wire slot a transmission filled (its six words); the other slots are
-    // unchanged, so a link state built from the fields alone (link_from_words) writes back right
+    // the fields, and the wire slot a transmission filled (its six words; the other slots are
+    // unchanged)
     const uint32_t ws = j - LR_WT;
-    if (j < LR_PMLO || (k.wmod != ~0u && j >= LR_WT && ws < (3u + kMemAux) * R.WCAP && (ws & (R.WCAP - 1u)) == k.wmod))
+    if (j < LR_PMLO || (k.wmod != ~0u && j >= LR_WT && ws < 3u * R.WCAP && (ws & (R.WCAP - 1u)) == k.wmod))
         R.lrec[l * R.RW + j] = w;
+    if (k.wmod != ~0u && j >= 4u * k.wmod && j < 4u * k.wmod + kMemAux) R.laux[l * R.AW + j] = k.aux;
     // next event of the link (register-resident link_put's rule)
     const uint32_t n0 = lo32(H.now);
     uint32_t t = 0, s = 0xffffffffu, kind = 0;
@@ -268,9 +257,7 @@ __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, u
         if (kind == 0 || rw < rt || (rw == rt && k.wh_seq < s)) { t = k.wh_t; s = k.wh_seq; kind = K_ARRIVE; }
     }
     const int64_t at = kind ? H.now + (int64_t)(uint32_t)(t - n0) : kInf;
-    // the kind byte carries the wire head's prefetch class (code bits 30-31) for an arrival
-    const uint32_t kb = kind == K_ARRIVE ? (kind | (k.hint << 2)) : kind;
-    tree_touch(S, R, H, l, at, s, (kb << 28) | l, kb);
+    tree_touch(S, R, H, l, at, s, (kind << 28) | l, kind);
 }
 
 // ---- flows ----
@@ -377,48 +364,20 @@ __device__ __forceinline__ void select_event(const Sim& S, const MemSt& R, const
 }
 
 // ---------------------------------------------------------------------------
-// arrival (engine_core.h on_arrive, identity overlays) with the prefetch of its hint class:
-// the link record, and with it -- in one HBM round trip --
-//   kHintDecide: words 0-7 and the ping words of every out-link of the deciding node (its
-//     observation, and the chosen out-link's state for the send: no load after the decision),
-//     and (MLP instances) every weight of the decision but the one-hot row element, which
-//     follows as soon as the record names the destination;
-//   kHintPing: the record, ping window and ping-back delay slots of the link back to the
-//     sender (a ping-forward's answer goes out on it, a ping-back acknowledges its tunnel);
-//   kHintDest: nothing.
-// A forwarded packet's previous decision (time, uid, node | destination | start second) comes
-// from the wire slot's aux words (engine_layout.h kMemAux), not from the decision log.
+// arrival (engine_core.h on_arrive, identity overlays).  A forwarded packet's previous decision
+// (time, uid, node | destination | start second) comes from the wire slot's aux words
+// (engine_layout.h kMemAux), not from the decision log, so an arrival waits for one HBM round
+// trip (the link record) before the decision's observation gather and layer 1-2 weights go out.
 // ---------------------------------------------------------------------------
 template <bool MLPK, class RS>
-__device__ __forceinline__ int on_arrive_mem(const Sim& S, RS& R, Hot& H, uint32_t l, uint32_t hint, Decision& D,
-                                             bool fused, MlpPre1& Mp, ArrPre& A) {
+__device__ __forceinline__ int on_arrive_mem(const Sim& S, RS& R, Hot& H, uint32_t l, Decision& D, bool fused,
+                                             MlpPre1& Mp, bool& pre) {
     static_assert(RS::kMem, "memory-resident engine only");
     const LV& L = S.lv;
     const int lane = S.lane;
     const uint32_t v = (uint32_t)t_ldst(S, l);
-    const uint32_t rec = rec_load(R, l);                            // issued first
-    A.out = false; A.mlp = false; A.ping = false; A.pop = false;
-    if (hint == kHintDecide) {
-        const int r0 = t_ovrow(S, v), deg = t_ovrow(S, v + 1) - r0;
-        const bool act = lane >= 1 && lane <= deg;
-        const uint32_t* p = R.lrec + (uint32_t)(r0 + (act ? lane - 1 : 0)) * R.RW;
-#pragma unroll
-        for (int w = 0; w < 8; ++w) A.o[w] = p[w];
-        A.pw[0] = p[LR_PMLO]; A.pw[1] = p[LR_PAVLO]; A.pw[2] = p[LR_PAVHI]; A.pw[3] = p[LR_ODLO]; A.pw[4] = p[LR_ODHI];
-        A.out = true;
-        if constexpr (MLPK) {
-            mlp_preload_all(Mp, S, v);
-            A.mlp = true;
-        }
-    } else if (hint == kHintPing) {
-        const uint32_t lr = (uint32_t)t_lrev(S, l);
-        A.prec = rec_load(R, lr);
-        A.pwin = (uint32_t)lane < L.ma() ? ((const uint32_t*)S.win)[lr * L.ma() + (uint32_t)lane] : 0u;
-        A.ppbd = (uint32_t)lane < L.PBK() ? ((const uint32_t*)S.pbd)[lr * L.PBK() + (uint32_t)lane] : 0u;
-        A.ping = true;
-    }
-    if constexpr (true) TM_WAIT(0);
-    LinkV k = link_from_rec(R, l, rec);
+    LinkV k = link_get_aux(R, l);
+    TM_WAIT(0);
     const uint32_t wh = k.head & (uint32_t)(L.WCAP() - 1);
     const uint32_t x = wire_ent(S, k, wh);
     const uint32_t type = ent_type(x);
@@ -427,14 +386,31 @@ __device__ __forceinline__ int on_arrive_mem(const Sim& S, RS& R, Hot& H, uint32
         const uint32_t a0 = wire_aux(S, k, wh, 0u), a1 = wire_aux(S, k, wh, 1u), a2 = wire_aux(S, k, wh, 2u);
         const uint32_t d = H.dec;
         const uint32_t dist = (d - r_dec(x)) & kRelayMask;
+        const bool fresh = type == T_FRESH;
+        const uint32_t dst = fresh ? f_dst(x) : ((a2 >> 8) & 255u);
+        // the decision's inputs go out first: the observation gather over node v's out-links
+        // (nothing touches them before the decision) and its layer 1-2 weights
+        if constexpr (MLPK && PRISMA_MEM_W_EARLY) {
+            if (fused && dst != v) {
+                if (PRISMA_MEM_W_EARLY == 3) mlp_preload_l1(Mp, S, v);
+                else mlp_preload_l12(Mp, S, v);
+                Mp.w1v = mlp_row_elem(S, v, dst);
+                pre = true;
+            }
+        }
+        // (table policy: the action table's entry goes out with the gather, not after it)
+        int tab = 0;
+        if constexpr (!MLPK) {
+            if (fused && dst != v) tab = table_action(S, v * (uint32_t)L.N() + dst);
+        }
+        const uint32_t obs_links = observe_links(S, R, H, v, ns_to_sec(H.now));
         double reward = 0.0;
         int32_t prev = -1;
-        uint32_t dst, start, uid, last = 0u;
-        if (type == T_FRESH) {
+        uint32_t start, uid, last = 0u;
+        if (fresh) {
             // first notification: destination from the flow, uid and start second rebuilt from
             // their low bits (the packet left its app less than 1 s and fewer than 2^20
             // injections ago)
-            dst = f_dst(x);
             const uint32_t s0 = (uint32_t)(TSEC(H.now));
             start = s0 - ((s0 ^ f_parity(x)) & 1u);
             const uint32_t lu = H.uid - 1u;
@@ -445,37 +421,13 @@ __device__ __forceinline__ int on_arrive_mem(const Sim& S, RS& R, Hot& H, uint32
             prev = (int32_t)(d - dist);
             if (dist >= L.log_cap()) fail(H, PRISMA_EBIT_LOGWRAP);
             uid = a1;
-            dst = (a2 >> 8) & 255u;
             start = a2 >> 16;
             last = a2 & 255u;
             const int64_t t_prev = H.now - (int64_t)(uint32_t)(lo32(H.now) - a0);
             reward = (double)py_micros(H.now) / 1e6 - (double)py_micros(t_prev) / 1e6;   // forwarder.py:360
             CNT_ADD(S, reward_sum, reward);
         }
-        if constexpr (MLPK) {                                       // the one-hot row element
-            if (A.mlp && dst != v) {
-                Mp.w1v = mlp_row_elem(S, v, dst);
-                Mp.has_w1 = true;
-            }
-        }
-        uint32_t obs_links;
-        if (A.out) {
-            const bool act = lane >= 1 && lane <= t_ovrow(S, v + 1) - t_ovrow(S, v);
-            const uint32_t ob = L.ping_as_obs()
-                ? ping_value_lane(ld_d(A.pw[1], A.pw[2]), A.pw[0], ld_d(A.pw[3], A.pw[4]), H.ping_rounds,
-                                  ns_to_sec(H.now))
-                : A.o[LR_QB];
-            obs_links = act ? ob : 0u;
-        } else {
-            obs_links = observe_links(S, R, H, v, ns_to_sec(H.now));
-        }
-        if constexpr (true) TM_WAIT(1);
-        if (fused && dst != v) {                                    // popped after the decision
-            A.pop = true;
-            A.kl = k;
-        } else {
-            wire_pop(S, R, H, l, k);
-        }
+        wire_pop(S, R, H, l, k);
         H.dec = d + 1u;
         // obs[0] = m_map_overlay_array[dst] (the identity on identity overlays)
         const uint32_t o = (lane == 0) ? dst : obs_links;
@@ -485,6 +437,7 @@ __device__ __forceinline__ int on_arrive_mem(const Sim& S, RS& R, Hot& H, uint32
         const uint32_t echo = (S.ctrl && L.train() && v != ent_src(x, v)) ? PEND_ECHO : 0u;
         D.x = x; D.dst = dst; D.start = start; D.uid = uid; D.v = v; D.d = d; D.reward = reward; D.prev = prev;
         D.obs = o; D.flags = echo; D.last = last; D.ttl = 255u;        // SetIpTtl(255) (poisson-application.cc:330)
+        D.tab = tab;
         if (dst == v) {                                             // getGameOver
             write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_DESTINATION, o, 255u);
             if (!fused && S.ctrl && L.notify_dest()) {              // the agent is notified (done=True)
@@ -529,24 +482,16 @@ __device__ __forceinline__ int on_arrive_mem(const Sim& S, RS& R, Hot& H, uint32
         receive_counters(S, R, H, x, false, 0u, l);
         return 0;
     }
-    // pings (identity overlays: tunnel == link, every node an overlay node; ping-forward on
-    // link t arrives over t itself, a ping-back for tunnel t over the reverse of t)
+    // pings (identity overlays: tunnel == link, every node an overlay node; a ping-forward on
+    // link t arrives over t itself, the ping-back for tunnel t over the reverse of t)
     const uint32_t t = p_tunnel(x), rnd = p_round(x);
     if (type == T_PFWD) {                                           // ping-forward-packet-manager.cc:94-156
         const float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
         st_rep(S, &S.pbd[t * L.PBK() + (rnd & (L.PBK() - 1))], delay);
-        const uint32_t lr = (uint32_t)t_lrev(S, l);
-        const uint32_t pb = p_make(T_PBACK, t, 0u, rnd);
-        const int ok = A.ping ? link_send_k(S, R, H, lr, pb, link_from_rec(R, lr, A.prec)) : link_send(S, R, H, lr, pb);
-        if (!ok) CNT_ADD(S, ctrl_dropped, 1u);
+        if (!link_send(S, R, H, (uint32_t)t_lrev(S, l), p_make(T_PBACK, t, 0u, rnd))) CNT_ADD(S, ctrl_dropped, 1u);
     } else {                                                        // ping-back-packet-manager.cc:120-144
-        if (A.ping) {
-            const float delay = __uint_as_float(rdl(A.ppbd, rnd & (L.PBK() - 1)));
-            ping_ack<true>(S, R, H, t, rnd, delay, A.prec, A.pwin);
-        } else {
-            const float delay = __uint_as_float(u_ld32((const uint32_t*)S.pbd + t * L.PBK() + (rnd & (L.PBK() - 1))));
-            ping_ack(S, R, H, t, rnd, delay);
-        }
+        const float delay = __uint_as_float(u_ld32((const uint32_t*)S.pbd + t * L.PBK() + (rnd & (L.PBK() - 1))));
+        ping_ack(S, R, H, t, rnd, delay);
     }
     receive_counters(S, R, H, x, false, 0u, l);
     return 0;
@@ -595,6 +540,8 @@ __device__ __forceinline__ void mem_bind(Sim& S, MemSt& R, const KParams& P, con
     R.n2 = LC.n2;
     R.RW = LC.lrec_words;
     R.WCAP = (uint32_t)LC.WCAP;
+    R.laux = (uint32_t*)(img + LC.g_laux);
+    R.AW = 4u * (uint32_t)LC.WCAP;
     R.fblk = make_uint4(0u, 0u, 0u, 0u);
     R.fblk_b = ~0u;
 }

@@ -287,9 +287,12 @@ class PrismaEngine:
         for step(); replicas without a pending decision get `fill`."""
         import torch
         out = torch.empty(self.R, dtype=torch.int32, device=self.torch_device)
-        cnt = torch.tensor([int(ids.numel())], dtype=torch.int32, device=self.torch_device)
-        ids_c = ids.to(torch.int32).contiguous()
-        act = packed_actions.to(torch.int32).contiguous()
+        n = int(ids.numel())
+        cnt = torch.tensor([n], dtype=torch.int32, device=self.torch_device)
+        # (an empty batch still passes valid device pointers: the count says there is nothing)
+        ids_c = ids.to(torch.int32).contiguous() if n else torch.zeros(1, dtype=torch.int32, device=self.torch_device)
+        act = (packed_actions.to(torch.int32).contiguous() if n
+               else torch.zeros(1, dtype=torch.int32, device=self.torch_device))
         _check(_lib.prisma_expand_actions(self.h, ids_c.data_ptr(), cnt.data_ptr(), act.data_ptr(), int(fill),
                                           out.data_ptr(), _stream_handle(stream)))
         return out
