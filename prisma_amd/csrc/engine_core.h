@@ -50,15 +50,11 @@ static __device__ unsigned int g_prisma_trace_cap;
 static __device__ unsigned int g_prisma_trace_n[8];
 #endif
 #if PRISMA_TIMING
-static __device__ unsigned long long g_prisma_timing[48];   // one copy per engine (translation unit); 16-19: mlp_action phases
+static __device__ unsigned long long g_prisma_timing[32];   // one copy per engine (translation unit); 16-19: mlp_action phases
 #define TM_NOW() ((uint64_t)__builtin_amdgcn_s_memtime())
 #define TM_FLOW(i) do { const uint64_t t_ = TM_NOW(); S.tflow[i] += t_ - S.tfl; S.tfl = t_; } while (0)
-// wait probe: cycles an explicit full wait takes at this point (what is still in flight)
-#define TM_WAIT(i) do { const uint64_t a_ = TM_NOW(); __builtin_amdgcn_s_waitcnt(0); \
-                        const uint64_t b_ = TM_NOW(); S.twait[i] += b_ - a_; S.nwait[i]++; } while (0)
 #else
 #define TM_FLOW(i) do { } while (0)
-#define TM_WAIT(i) do { } while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -326,7 +322,6 @@ struct Sim {
     mutable uint64_t tsub[2], tlast;             // sub-phase cycles inside apply_decision
     mutable uint64_t tmlp[4];                    // mlp_action phases (timing build)
     mutable uint64_t tflow[4], tfl;              // memory-resident on_flow phases (timing build)
-    mutable uint64_t twait[6]; mutable uint32_t nwait[6];   // wait probes (TM_WAIT)
 #endif
 };
 
@@ -402,30 +397,6 @@ __device__ __forceinline__ void st_rep(const Sim& S, T* p, T v) {
 // a dequeue behind a busy transmitter reads the ring back).
 __device__ __forceinline__ void ring_put(const Sim& S, uint32_t i, uint32_t e) {
     S.ring[i] = e;
-}
-
-// memory-resident engine: 16-B FIFO slots {entry, aux0, aux1, aux2} (engine_layout.h kMemAux)
-#ifndef PRISMA_RING4_LANES
-#define PRISMA_RING4_LANES 0
-#endif
-// memory-resident engine: which of a decision's weights go out with the arrival's observation
-// gather (A/B): 3 layer 1 (layers 2-4 when the decision starts), 1 layers 1-2,
-// 0 none (all at the decision)
-#ifndef PRISMA_MEM_W_EARLY
-#define PRISMA_MEM_W_EARLY 0
-#endif
-__device__ __forceinline__ void ring_put4(const Sim& S, uint32_t i, uint4 e) {
-    if (PRISMA_RING4_LANES) {                    // (A/B variant) lanes 0-3 store one word each
-        const uint32_t j = (uint32_t)S.lane;
-        const uint32_t w = j == 0 ? e.x : (j == 1 ? e.y : (j == 2 ? e.z : e.w));
-        if (j < 4) ((uint32_t*)S.ring)[4u * i + j] = w;
-    } else {
-        ((uint4*)S.ring)[i] = e;
-    }
-}
-__device__ __forceinline__ uint4 ring_get4(const Sim& S, uint32_t i) {
-    const uint4 v = ((const uint4*)S.ring)[i];
-    return make_uint4(rfl(v.x), rfl(v.y), rfl(v.z), rfl(v.w));
 }
 
 // uniform LDS reads (every lane reads the same address: broadcast, no conflict)
@@ -514,9 +485,6 @@ struct LinkV {
     uint32_t cp_t, cp_seq;       // completion time (low 32 bits), seq
     uint32_t wh_t, wh_seq;       // wire-head arrival time (low 32 bits), seq
     uint32_t rec;                // memory-resident engine: the link's record, lane j = word j
-    uint32_t wmod;               // memory-resident: wire slot written since the load (~0: none)
-    uint32_t aux;                // memory-resident: the link's wire aux block, lane 4i + m = aux word m
-                                 // of slot i (loaded by arrivals; written for the slot wmod)
 };
 
 template <int FS, int LS>
@@ -661,23 +629,12 @@ __device__ __forceinline__ void ping_set_win(const Sim& S, Regs<FS, LS>& R, uint
 // engine -- the packet entry.  Register-resident: LDS arrays; memory-resident: words
 // LR_WT + {i, WCAP + i, 2 WCAP + i} of the link record held in k.rec (written back by
 // link_put), so an arrival reads its packet without a ring access.
-// (memory-resident: and the entry's aux words, engine_layout.h kMemAux)
 __device__ __forceinline__ void wire_set(const Sim& S, LinkV& k, uint32_t l, uint32_t i, uint32_t t, uint32_t s,
-                                         uint32_t x, uint4 ax = uint4{}) {
+                                         uint32_t x) {
     const uint32_t W = (uint32_t)S.lv.WCAP();
     if (S.mem) {
         const uint32_t j = (uint32_t)S.lane;
-        uint32_t v = k.rec;
-        v = j == LR_WT + i ? t : v;
-        v = j == LR_WT + W + i ? s : v;
-        v = j == LR_WT + 2u * W + i ? x : v;
-        k.rec = v;
-        uint32_t a = k.aux;
-        a = j == 4u * i ? ax.y : a;
-        a = j == 4u * i + 1u ? ax.z : a;
-        a = j == 4u * i + 2u ? ax.w : a;
-        k.aux = a;
-        k.wmod = i;
+        k.rec = j == LR_WT + i ? t : (j == LR_WT + W + i ? s : (j == LR_WT + 2u * W + i ? x : k.rec));
     } else {                                  // every lane stores the same value to the same address:
         S.wt[l * W + i] = t;                  // no exec-mask juggling (A/B +1 % against lane 0 only)
         S.wseq[l * W + i] = s;
@@ -698,13 +655,10 @@ __device__ __forceinline__ void wire_get(const Sim& S, const LinkV& k, uint32_t 
 __device__ __forceinline__ uint32_t wire_ent(const Sim& S, const LinkV& k, uint32_t i) {
     return rdl(k.rec, LR_WT + 2u * (uint32_t)S.lv.WCAP() + i);
 }
-// memory-resident engine: aux word m (< kMemAux) of wire slot i (the arrival's aux block load)
-__device__ __forceinline__ uint32_t wire_aux(const Sim& S, const LinkV& k, uint32_t i, uint32_t m) {
-    return rdl(k.aux, 4u * i + m);
-}
+
 // ---- link FIFO / transmitter (point-to-point-net-device.cc:273-336, 595-666)
 __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l, LinkV& k, uint32_t ring_idx,
-                                               uint32_t x, uint4 ax = uint4{}) {
+                                               uint32_t x) {
     const LV& L = S.lv;
     const bool sw = l < (uint32_t)L.E();
     x = rfl(x);                  // uniform entry: its class indexes the topology image with a scalar load
@@ -725,7 +679,7 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
     const uint32_t w = ring_idx & (uint32_t)(L.WCAP() - 1);
     const uint32_t at = lo32(H.now + tx + prop);
     const uint32_t as = H.seq++;                               // channel Receive
-    wire_set(S, k, l, w, at, as, x, ax);
+    wire_set(S, k, l, w, at, as, x);
     if (k.n_wire == 1) { k.wh_t = at; k.wh_seq = as; }        // the wire was empty: new head
     if (k.n_wire > (uint32_t)L.WCAP()) fail(H, PRISMA_EBIT_WIRE);
 }
@@ -735,8 +689,7 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
 // issues the record load early); the register-resident engine keeps the plain form below,
 // whose register allocation the by-value LinkV disturbs
 template <class RS>
-__device__ __forceinline__ int link_send_k(const Sim& S, RS& R, Hot& H, uint32_t l, uint32_t e, LinkV k,
-                                           uint4 ax = uint4{}) {
+__device__ __forceinline__ int link_send_k(const Sim& S, RS& R, Hot& H, uint32_t l, uint32_t e, LinkV k) {
     const LV& L = S.lv;
     uint32_t size = ent_size(S, e, l);
     bool ok = l < (uint32_t)L.E() ? (k.qb + size <= L.qmax_bytes()) : (k.n_queue + 1u <= L.acc_qmax_pkts());
@@ -750,36 +703,26 @@ __device__ __forceinline__ int link_send_k(const Sim& S, RS& R, Hot& H, uint32_t
     }
     uint32_t cap = ring_cap(S, l), off = ring_off(S, l);
     if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
-    if constexpr (RS::kMem) ring_put4(S, off + k.tail, make_uint4(e, ax.y, ax.z, ax.w));
-    else ring_put(S, off + k.tail, e);
+    ring_put(S, off + k.tail, e);
     k.tail = (k.tail + 1 == cap) ? 0 : k.tail + 1;
     k.n_queue++;
     k.qb += size;
     if (!k.busy) {                                              // :643-650
         uint32_t xi = k.txp;
-        uint32_t hx;
-        uint4 h4 = ax;
-        if constexpr (RS::kMem) {
-            // (the queue was empty behind an idle transmitter: the head is this packet)
-            if (k.n_queue != 1) h4 = ring_get4(S, off + xi);
-            hx = k.n_queue == 1 ? e : h4.x;
-        } else {
-            hx = (k.n_queue == 1) ? e : u_ld32(&S.ring[off + xi]);
-        }
+        uint32_t hx = (k.n_queue == 1) ? e : u_ld32(&S.ring[off + xi]);
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
         k.qb -= ent_size(S, hx, l);
-        transmit_start(S, H, l, k, xi, hx, h4);
+        transmit_start(S, H, l, k, xi, hx);
     }
     link_put(S, R, H, l, k);
     return 1;
 }
 template <class RS>
-__device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l, uint32_t e, uint4 ax = uint4{}) {
+__device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l, uint32_t e) {
     const LV& L = S.lv;
     LinkV k = link_get(R, l);
-    if constexpr (RS::kMem) TM_WAIT(2);
     uint32_t size = ent_size(S, e, l);
     bool ok = l < (uint32_t)L.E() ? (k.qb + size <= L.qmax_bytes()) : (k.n_queue + 1u <= L.acc_qmax_pkts());
     if (!ok) return 0;
@@ -792,27 +735,18 @@ __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l
     }
     uint32_t cap = ring_cap(S, l), off = ring_off(S, l);
     if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
-    if constexpr (RS::kMem) ring_put4(S, off + k.tail, make_uint4(e, ax.y, ax.z, ax.w));
-    else ring_put(S, off + k.tail, e);
+    ring_put(S, off + k.tail, e);
     k.tail = (k.tail + 1 == cap) ? 0 : k.tail + 1;
     k.n_queue++;
     k.qb += size;
     if (!k.busy) {                                              // :643-650
         uint32_t xi = k.txp;
-        uint32_t hx;
-        uint4 h4 = ax;
-        if constexpr (RS::kMem) {
-            // (the queue was empty behind an idle transmitter: the head is this packet)
-            if (k.n_queue != 1) h4 = ring_get4(S, off + xi);
-            hx = k.n_queue == 1 ? e : h4.x;
-        } else {
-            hx = (k.n_queue == 1) ? e : u_ld32(&S.ring[off + xi]);
-        }
+        uint32_t hx = (k.n_queue == 1) ? e : u_ld32(&S.ring[off + xi]);
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
         k.qb -= ent_size(S, hx, l);
-        transmit_start(S, H, l, k, xi, hx, h4);
+        transmit_start(S, H, l, k, xi, hx);
     }
     link_put(S, R, H, l, k);
     return 1;
@@ -823,25 +757,16 @@ template <class RS>
 __device__ __forceinline__ void on_complete(const Sim& S, RS& R, Hot& H, uint32_t l) {   // :305-336
     const LV& L = S.lv;
     LinkV k = link_get(R, l);
-    if constexpr (RS::kMem) TM_WAIT(3);
     k.busy = 0;
     if (k.n_queue) {
         uint32_t cap = ring_cap(S, l);
         uint32_t xi = k.txp;
-        uint32_t hx;
-        uint4 h4 = uint4{};
-        if constexpr (RS::kMem) {
-            h4 = ring_get4(S, ring_off(S, l) + xi);
-            hx = h4.x;
-        } else {
-            hx = u_ld32(&S.ring[ring_off(S, l) + xi]);
-        }
-        if constexpr (RS::kMem) TM_WAIT(4);
+        uint32_t hx = u_ld32(&S.ring[ring_off(S, l) + xi]);
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
         k.qb -= ent_size(S, hx, l);
-        transmit_start(S, H, l, k, xi, hx, h4);
+        transmit_start(S, H, l, k, xi, hx);
     }
     link_put(S, R, H, l, k);
 }
@@ -1025,10 +950,7 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
         // source, engine_layout.h)
         const uint32_t src = (RS::kMem && !S.ctrl) ? dst : ent_src(x, v);
         const uint32_t fwd = (PRISMA_ABLATE & 1) ? (T_RELAY | (dst << 2) | (start << 10) | (src << 24)) : r_make(d, src);
-        // memory-resident: the decision's time, uid and record word 6 ride with the packet
-        const uint4 ax = make_uint4(0u, lo32(H.now), uid, v | (dst << 8) | (start << 16));
-        const int sent = RS::kMem ? link_send(S, R, H, l, fwd, ax) : link_send(S, R, H, l, fwd);
-        if (sent) {                                               // lastHop = v, previous decision = d
+        if (link_send(S, R, H, l, fwd)) {                         // lastHop = v, previous decision = d
             status = PRISMA_ST_ENQUEUED;
         } else {
             status = PRISMA_ST_DROPPED;              // :655-664 + forwarder.py:214-244
@@ -1071,9 +993,7 @@ __device__ __forceinline__ int finish_pending(const Sim& S, RS& R, Hot& H, int a
         receive_counters(S, R, H, x, true, u_ld32(&h.pend_ent[2]), 0u);
         return 0;
     }
-    // (destination and start second: the memory-resident engine's relay aux words carry them)
-    apply_decision(S, R, H, x, RS::kMem ? u_ld32(&h.pend_ent[1]) : 0u, RS::kMem ? u_ld32(&h.pend_ent[2]) : 0u,
-                   u_ld32(&h.pend_uid), u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action,
+    apply_decision(S, R, H, x, 0u, 0u, u_ld32(&h.pend_uid), u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action,
                    false, 0.0, 0, 0u, echo_link, last, 0u);
     return 1;
 }
@@ -1206,7 +1126,6 @@ __device__ __forceinline__ void on_flow(const Sim& S, RS& R, Hot& H, uint32_t f)
         const uint32_t acc = (uint32_t)S.lv.E() + (uint32_t)t_fsrc(S, f);
         const LinkV k = link_get(R, acc);
         draw = flow_draw(S, R, f);
-        TM_WAIT(5);
         TM_FLOW(0);
         if (draw != 0) {                                            // SendPacket :297-358
             const uint32_t par = (uint32_t)(TSEC(H.now)) & 1u;          // start second (its parity)
@@ -1289,9 +1208,6 @@ struct MlpPre1 {
     float b1v;
     float w1v;                   // the one-hot row element, when the destination was known (has_w1)
     bool has_w1;
-    // (mlp_action PRE == 2, the memory-resident engine) the buffer-branch chunks 4-7 (degrees
-    // 17-32) too
-    float4 wx[4];
 };
 
 __device__ __forceinline__ void mlp_preload(MlpPre& M, const float* __restrict__ RP, int lane, int D, int deg,
@@ -1338,54 +1254,6 @@ __device__ __forceinline__ void mlp_preload_node(MlpPre1& M, const Sim& S, uint3
 #pragma unroll
     for (int c = 0; c < 4; ++c) M.wb[c] = (c < nck) ? Wb4[c * 32 + j32] : make_float4(0.f, 0.f, 0.f, 0.f);
     M.b1v = (lane < 32) ? RP1[128 * ((D + 3) / 4) + 32 + j32] : RP1[128 * ((D + 3) / 4) + j32];
-}
-
-// layer 1 of a decision at node v (buffer branch chunks 0-7 and biases) for mlp_action PRE 3
-__device__ __forceinline__ void mlp_preload_l1(MlpPre1& M, const Sim& S, uint32_t v) {
-    const int lane = S.lane;
-    v = rfl(v);
-    const int D = S.lv.max_deg();
-    const float* __restrict__ RP1 = S.mlp_rp + (size_t)v * mlp_rp_node_floats(D);
-    const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
-    const int j32 = lane & 31, nck = (deg + 3) >> 2;
-    const float4* __restrict__ Wb4 = (const float4*)RP1;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) M.wb[c] = Wb4[(c < nck ? c : 0) * 32 + j32];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) M.wx[c] = Wb4[((c + 4 < nck) ? c + 4 : 0) * 32 + j32];
-    M.b1v = (lane < 32) ? RP1[128 * ((D + 3) / 4) + 32 + j32] : RP1[128 * ((D + 3) / 4) + j32];
-}
-
-// the one-hot row element W1[v][dst][j] of lane j < 32 (models.py:258-306's one-hot branch)
-__device__ __forceinline__ float mlp_row_elem(const Sim& S, uint32_t v, uint32_t dst) {
-    return S.lane < 32 ? S.mlp[((int)rfl(v) * S.lv.N() + (int)rfl(dst)) * 32 + (S.lane & 31)] : 0.0f;
-}
-// layers 1-2 of a decision at node v (buffer branch with chunks 4-7, biases, layer 2) for
-// mlp_action PRE 2; the memory-resident engine issues them with the arrival's observation
-// gather as soon as the link record shows a packet to decide on (mlp_row_elem adds the one-hot
-// row element).  Layers 3-4 load when the decision starts (mlp_action): they are first needed
-// two layers later.
-__device__ __forceinline__ void mlp_preload_l12(MlpPre1& M, const Sim& S, uint32_t v) {
-    const int lane = S.lane;
-    v = rfl(v);
-    const int D = S.lv.max_deg();
-    const float* __restrict__ RP1 = S.mlp_rp + (size_t)v * mlp_rp_node_floats(D);
-    const float* __restrict__ RP = RP1 + mlp_rp_l1_floats(D);
-    const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
-    M.has_w1 = false;
-    M.w1v = 0.0f;
-    const int j32 = lane & 31, nck = (deg + 3) >> 2;
-    const float4* __restrict__ Wb4 = (const float4*)RP1;
-    // (chunks past the degree read chunk 0 again: every load unconditional, so the in-order
-    // load counter is waited on exactly)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) M.wb[c] = Wb4[(c < nck ? c : 0) * 32 + j32];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) M.wx[c] = Wb4[((c + 4 < nck) ? c + 4 : 0) * 32 + j32];
-    M.b1v = (lane < 32) ? RP1[128 * ((D + 3) / 4) + 32 + j32] : RP1[128 * ((D + 3) / 4) + j32];
-#pragma unroll
-    for (int c = 0; c < 16; ++c) M.w2[c] = ((const float4*)RP)[c * 64 + lane];
-    M.b2 = RP[64 * 64 + lane];
 }
 
 __device__ __forceinline__ float mlp_dense64_pre(const Sim& S, const float4 (&w)[16], float b) {
@@ -1517,10 +1385,7 @@ __device__ __forceinline__ int lane_argmin_first(float q, int n) {
     return (int)__builtin_ctzll(__ballot(key == kmin));
 }
 
-// PRE: 0 every weight loaded here; 1 (memory-resident arrival) layers 1-2 in P1 and, when
-// P1.has_w1, the one-hot row element; 2 layers 1-2 with buffer chunks 4-7 and the row element in
-// P1; 3 layer 1 (chunks 0-7, bias, row element) in P1, layers 2-4 loaded here
-template <int B, int PRE = 0>
+template <int B, bool PRE = false>
 __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs_reg, const MlpPre1& P1) {
     const LV& L = S.lv;
     const int lane = S.lane;
@@ -1550,16 +1415,14 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     const int nck = (deg + 3) >> 2;
     const float4* __restrict__ Wb4 = (const float4*)RP1;
     float w1v;
-    if (PRE >= 2 || (PRE && P1.has_w1)) w1v = P1.w1v;
+    if (PRE && P1.has_w1) w1v = P1.w1v;
     else w1v = (lane < 32) ? W1[((int)v * N + (int)dst) * 32 + j32] : 0.0f;
     // memory-resident engine: buffer-branch chunks 4-7 (degrees 17-32) are loaded here, BEFORE
     // the layer 3-4 stream: the load counter is in order, so a chunk loaded inside layer 1
     // made layer 1 wait for the whole stream (and the compiler, unable to count the loop's
     // loads, waited for everything before layer 2)
     float4 wx[4];
-    if constexpr (B == kMlpAll && PRE >= 2) {
-        // (chunks 4-7 in P1: used in place below)
-    } else if constexpr (B == kMlpAll) {
+    if constexpr (B == kMlpAll) {
         // (always issued, chunk 0 again past the node's degree: no branch for the scheduler to
         // hoist the stream's loads above)
 #pragma unroll
@@ -1567,13 +1430,10 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
         __builtin_amdgcn_sched_barrier(0);
     }
     MlpPre M;
-    // (PRE 1, 2: layer 2 came with the arrival)
-    if constexpr (B == kMlpAll) mlp_preload(M, RP, lane, D, deg, PRE == 0 || PRE == 3);
+    if constexpr (B == kMlpAll) mlp_preload(M, RP, lane, D, deg, !PRE);   // PRE: layer 2 came with the arrival
     float b1v;
     float4 wb[4];
-    if constexpr (PRE >= 2) {
-        b1v = P1.b1v;
-    } else if constexpr (PRE) {
+    if constexpr (PRE) {
         b1v = P1.b1v;
 #pragma unroll
         for (int c = 0; c < 4; ++c) wb[c] = P1.wb[c];
@@ -1619,12 +1479,8 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     if constexpr (B == kMlpAll) {
         // chunks named at compile time (a runtime-indexed select over wb/wx put them on the stack)
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-            if (c < nck) {
-                if constexpr (PRE >= 2) chunk(c, c < 4 ? P1.wb[c & 3] : P1.wx[c & 3]);
-                else chunk(c, c < 4 ? wb[c & 3] : wx[c & 3]);
-            }
-        }
+        for (int c = 0; c < 8; ++c)
+            if (c < nck) chunk(c, c < 4 ? wb[c & 3] : wx[c & 3]);
         for (int c = 8; c < nck; ++c) chunk(c, Wb4[c * 32 + j32]);
     } else {
         for (int c = 0; c < nck; ++c) {
@@ -1647,7 +1503,7 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
         __builtin_amdgcn_wave_barrier();
         return lane_argmin_first_seq(q4, deg);
     }
-    if constexpr (PRE == 1 || PRE == 2) h = det_elu(mlp_dense64_pre(S, P1.w2, P1.b2));
+    if constexpr (PRE) h = det_elu(mlp_dense64_pre(S, P1.w2, P1.b2));
     else if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w2, M.b2));
     else h = det_elu(mlp_dense64<B>(S, RP, lane, 64));
     __builtin_amdgcn_wave_barrier();
@@ -1692,13 +1548,7 @@ __device__ __forceinline__ void wire_pop(const Sim& S, RS& R, const Hot& H, uint
 
 struct Decision {
     uint32_t x, dst, start, uid, v, d; double reward; int32_t prev; uint32_t obs, flags, last, ttl;
-    int tab;                     // memory-resident table policy: the action, read with the observation
 };
-
-// the memory-resident engine's arrival (prisma_engine_mem.hip)
-template <bool MLPK, class RS>
-__device__ __forceinline__ int on_arrive_mem(const Sim& S, RS& R, Hot& H, uint32_t l, Decision& D, bool fused,
-                                             MlpPre1& Mp, bool& pre);
 
 // a control packet (or a data packet inside a tunnel) continues along the
 // underlay route to `to` (Ipv4L3Protocol::IpForward through the patched
@@ -1777,7 +1627,6 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
     const LV& L = S.lv;
     const uint32_t v = (uint32_t)t_ldst(S, l);
     LinkV k = link_get(R, l);
-    if constexpr (RS::kMem) TM_WAIT(0);
     const uint32_t wh = k.head & (uint32_t)(L.WCAP() - 1);
     const uint32_t x = S.mem ? wire_ent(S, k, wh)
                              : (S.tun ? u_ld32(&S.went[l * (uint32_t)L.WCAP() + wh])
@@ -1848,7 +1697,6 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
             ttl = ttl_prev - (ti_len(ti) - 1u);
         }
         H.dec = d + 1u;
-        if constexpr (RS::kMem) TM_WAIT(1);
         const uint32_t obs_links = S.mem ? obs_early : observe_links(S, R, H, v, ns_to_sec(H.now));
         const int64_t t_prev = mk64(rfl(ph.x), rfl(ph.y));
         const uint32_t uid_prev = rfl(ph.z), w_prev = rfl(pw.x);
@@ -2312,7 +2160,6 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
     S.tsub[0] = 0; S.tsub[1] = 0; S.tlast = 0;
     S.tmlp[0] = 0; S.tmlp[1] = 0; S.tmlp[2] = 0; S.tmlp[3] = 0;
     S.tflow[0] = 0; S.tflow[1] = 0; S.tflow[2] = 0; S.tflow[3] = 0; S.tfl = 0;
-    for (int i = 0; i < 6; ++i) { S.twait[i] = 0; S.nwait[i] = 0; }
 #define TM_MARK(i) do { tm_b = TM_NOW(); tm_acc[i] += tm_b - tm_a; tm_cnt[i]++; tm_a = tm_b; } while (0)
 #else
 #define TM_MARK(i) do { } while (0)
@@ -2347,27 +2194,13 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
         TM_MARK(0);
         if (kind == K_ARRIVE) {
             Decision D;
-            MlpPre1 Mp;                                  // (kPre) the decision's weights, fetched on arrival
-            bool pre = false;                            // (memory-resident) layers 1-2 already in Mp
-            int need;
-            if constexpr (RS::kMem) need = on_arrive_mem<MLP>(S, R, H, id, D, table_mode, Mp, pre);
-            else need = on_arrive<kPre>(S, R, H, id, D, table_mode, Mp);
+            MlpPre1 Mp;                                  // (kPre) the decision's first weights, fetched on arrival
+            const int need = on_arrive<kPre>(S, R, H, id, D, table_mode, Mp);
             TM_MARK(1);
             if (need) {
                 if (table_mode) {
-                    int a;
-                    if constexpr (RS::kMem && MLP) {
-                        if (!pre) {                      // (not issued with the arrival: now)
-                            if (PRISMA_MEM_W_EARLY == 3) mlp_preload_l1(Mp, S, D.v);
-                            else mlp_preload_l12(Mp, S, D.v);
-                            Mp.w1v = mlp_row_elem(S, D.v, D.dst);
-                        }
-                        a = mlp_action<MB, PRISMA_MEM_W_EARLY == 3 ? 3 : 2>(S, D.v, D.obs, Mp);
-                    } else if constexpr (RS::kMem) {
-                        a = D.tab;                       // (on_arrive_mem read it with the observation)
-                    } else {
-                        a = mlp_mode ? mlp_action<MB, kPre>(S, D.v, D.obs, Mp) : table_action(S, D.v * NN + D.dst);
-                    }
+                    const int a = mlp_mode ? mlp_action<MB, kPre>(S, D.v, D.obs, Mp)
+                                           : table_action(S, D.v * NN + D.dst);
                     apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, a, true,
                                    D.reward, D.prev, D.obs,
                                    (D.flags & PEND_ECHO) ? (uint32_t)t_lrev(S, id) : kNoLink, D.last, D.ttl);
@@ -2413,10 +2246,6 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
         }
         for (int i = 0; i < 4; ++i) atomicAdd(&g_prisma_timing[16 + i], (unsigned long long)S.tmlp[i]);
         for (int i = 0; i < 4; ++i) atomicAdd(&g_prisma_timing[20 + i], (unsigned long long)S.tflow[i]);
-        for (int i = 0; i < 6; ++i) {
-            atomicAdd(&g_prisma_timing[24 + i], (unsigned long long)S.twait[i]);
-            atomicAdd(&g_prisma_timing[32 + i], (unsigned long long)S.nwait[i]);
-        }
     }
 #endif
     if (!H.error) lazy_resolve(S, R, H, false);      // elided completions up to where the launch stopped

@@ -188,7 +188,6 @@ struct Layout {
     uint32_t n_leaf, n1, n2;     // event tree: leaves (links, then flows), level-1 / level-2 nodes
     uint32_t s_lv1, s_lv2;       // LDS offsets of the tree levels (16-B nodes)
     uint32_t g_lrec, g_keys;     // image offsets of the link records and the flow leaf keys
-    uint32_t g_laux;             // ... and of the links' wire aux blocks (4 * WCAP words per link)
     uint32_t lrec_words;         // words per link record (32 or 64)
     uint32_t s_lkey, s_lkind;    // LDS offsets of the link leaf keys (time lo, seq) and kinds (bytes)
     // topology image offsets (memory-resident engine; variable-size arrays)
@@ -226,14 +225,6 @@ enum : uint32_t {
     LR_PMLO, LR_PMMLO, LR_PMMHI, LR_PMWIN, LR_PAVLO, LR_PAVHI, LR_ODLO, LR_ODHI,
     LR_WT = 16,                  // wire slots: arrival time [WCAP], seq [WCAP], packet entry [WCAP]
 };
-// The memory-resident engine's FIFO slots are 16 B {entry, aux0, aux1, aux2}, and each link has
-// a wire aux block beside its record (4 words per wire slot, Layout::g_laux): a forwarded data
-// packet carries its previous decision's time (low 32 bits), uid and record word 6 (deciding
-// node | destination << 8 | start second << 16), so its arrival reads them with the link record
-// (two loads issued together) instead of from the decision log afterwards (one dependent HBM
-// round trip less per data arrival).  Kept out of the record, so the accesses that do not need
-// them -- completions, sends, flows -- still move 128-B records.
-constexpr uint32_t kMemAux = 3u;
 constexpr uint32_t kMemMaxWire = 16u;
 
 }  // namespace prisma

@@ -541,8 +541,7 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
     L.lds_state_bytes = (uint32_t)o;
     L.g_lrec = take(4u * L.lrec_words * (uint64_t)Lk);
     L.g_keys = take(16u * (uint64_t)FG);
-    L.g_laux = take(16u * (uint64_t)L.WCAP * (uint64_t)Lk);     // 4 words per wire slot (kMemAux + pad)
-    L.s_ring = take(16u * (uint64_t)ring_total);            // 16-B slots {entry, aux} (kMemAux)
+    L.s_ring = take(4u * (uint64_t)ring_total);
     L.s_win = take(4u * (uint64_t)E * L.MA);
     L.s_pbd = take(4u * (uint64_t)E * L.PBK);
     if (o >= (1ull << 32)) return set_err(PRISMA_ERR_CONFIG, "replica state above 4 GiB");

@@ -26,13 +26,12 @@ struct MemSt {
     static constexpr bool kLazy = true;          // empty-queue transmit completions elided (lazy_resolve)
     static constexpr bool kMem = true;
     uint32_t* lrec;              // [L][RW] link records (HBM)
-    uint32_t* laux;              // [L][AW] wire aux blocks (HBM, engine_layout.h kMemAux)
     uint4* fkeys;                // [F] flow leaf keys {t lo, t hi, seq, draw} (HBM)
     uint2* lkey;                 // LDS [L] link leaf keys {t lo, seq}: t = now + (t lo - lo32(now))
     uint8_t* lkind;              // LDS [L] link event kind (0: none, K_COMPLETE, K_ARRIVE)
     uint4* lv1;                  // LDS [n1] {t lo, t hi, seq, code}
     uint4* lv2;                  // LDS [n2]
-    uint32_t L, n_leaf, n1, n2, RW, WCAP, AW;
+    uint32_t L, n_leaf, n1, n2, RW, WCAP;
     // the 64-leaf block of the flow whose send event runs, loaded (one coalesced 1 KiB
     // load) by flow_draw for its draw index; flow_set re-reduces the block from it instead
     // of storing the new key and loading the block back (one HBM round trip per flow event)
@@ -204,9 +203,9 @@ __device__ __forceinline__ uint32_t rec_load(const MemSt& R, uint32_t l) {
     return j < R.RW ? R.lrec[l * R.RW + j] : 0u;
 }
 
-__device__ __forceinline__ LinkV link_from_rec(const MemSt& R, uint32_t l, uint32_t rec) {
+__device__ __forceinline__ LinkV link_get(const MemSt& R, uint32_t l) {
     LinkV k;
-    k.rec = rec;
+    k.rec = rec_load(R, l);
     const uint32_t p0 = rdl(k.rec, LR_P0), p1 = rdl(k.rec, LR_P1), p2 = rdl(k.rec, LR_P2);
     k.head = p0 & 0xffffu; k.txp = p0 >> 16;
     k.tail = p1 & 0xffffu; k.n_wire = p1 >> 16;
@@ -216,20 +215,9 @@ __device__ __forceinline__ LinkV link_from_rec(const MemSt& R, uint32_t l, uint3
     k.cp_seq = rdl(k.rec, LR_CPS);
     k.wh_t = rdl(k.rec, LR_WHT);
     k.wh_seq = rdl(k.rec, LR_WHS);
-    k.wmod = ~0u;
-    k.aux = 0u;
     return k;
 }
-__device__ __forceinline__ LinkV link_get(const MemSt& R, uint32_t l) { return link_from_rec(R, l, rec_load(R, l)); }
-// an arrival's link state: the record and the wire aux block, loaded together
-__device__ __forceinline__ LinkV link_get_aux(const MemSt& R, uint32_t l) {
-    const uint32_t j = threadIdx.x;
-    const uint32_t rec = rec_load(R, l);
-    const uint32_t aux = j < R.AW ? R.laux[l * R.AW + j] : 0u;
-    LinkV k = link_from_rec(R, l, rec);
-    k.aux = aux;
-    return k;
-}
+
 template <unsigned MASK = LP_ALL>                 // (the whole record is written back either way)
 __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, uint32_t l, const LinkV& k) {
     const uint32_t j = threadIdx.x;
@@ -242,12 +230,7 @@ __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, u
     w = j == LR_CPS ? k.cp_seq : w;
     w = j == LR_WHT ? k.wh_t : w;
     w = j == LR_WHS ? k.wh_seq : w;
-    // the fields, and the wire slot a transmission filled (its six words; the other slots are
-    // unchanged)
-    const uint32_t ws = j - LR_WT;
-    if (j < LR_PMLO || (k.wmod != ~0u && j >= LR_WT && ws < 3u * R.WCAP && (ws & (R.WCAP - 1u)) == k.wmod))
-        R.lrec[l * R.RW + j] = w;
-    if (k.wmod != ~0u && j >= 4u * k.wmod && j < 4u * k.wmod + kMemAux) R.laux[l * R.AW + j] = k.aux;
+    if (j < LR_PMLO || (j >= LR_WT && j < LR_WT + 3u * R.WCAP)) R.lrec[l * R.RW + j] = w;
     // next event of the link (register-resident link_put's rule)
     const uint32_t n0 = lo32(H.now);
     uint32_t t = 0, s = 0xffffffffu, kind = 0;
@@ -364,140 +347,6 @@ __device__ __forceinline__ void select_event(const Sim& S, const MemSt& R, const
 }
 
 // ---------------------------------------------------------------------------
-// arrival (engine_core.h on_arrive, identity overlays).  A forwarded packet's previous decision
-// (time, uid, node | destination | start second) comes from the wire slot's aux words
-// (engine_layout.h kMemAux), not from the decision log, so an arrival waits for one HBM round
-// trip (the link record) before the decision's observation gather and layer 1-2 weights go out.
-// ---------------------------------------------------------------------------
-template <bool MLPK, class RS>
-__device__ __forceinline__ int on_arrive_mem(const Sim& S, RS& R, Hot& H, uint32_t l, Decision& D, bool fused,
-                                             MlpPre1& Mp, bool& pre) {
-    static_assert(RS::kMem, "memory-resident engine only");
-    const LV& L = S.lv;
-    const int lane = S.lane;
-    const uint32_t v = (uint32_t)t_ldst(S, l);
-    LinkV k = link_get_aux(R, l);
-    TM_WAIT(0);
-    const uint32_t wh = k.head & (uint32_t)(L.WCAP() - 1);
-    const uint32_t x = wire_ent(S, k, wh);
-    const uint32_t type = ent_type(x);
-    if (ent_is_data(x)) {
-        // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
-        const uint32_t a0 = wire_aux(S, k, wh, 0u), a1 = wire_aux(S, k, wh, 1u), a2 = wire_aux(S, k, wh, 2u);
-        const uint32_t d = H.dec;
-        const uint32_t dist = (d - r_dec(x)) & kRelayMask;
-        const bool fresh = type == T_FRESH;
-        const uint32_t dst = fresh ? f_dst(x) : ((a2 >> 8) & 255u);
-        // the decision's inputs go out first: the observation gather over node v's out-links
-        // (nothing touches them before the decision) and its layer 1-2 weights
-        if constexpr (MLPK && PRISMA_MEM_W_EARLY) {
-            if (fused && dst != v) {
-                if (PRISMA_MEM_W_EARLY == 3) mlp_preload_l1(Mp, S, v);
-                else mlp_preload_l12(Mp, S, v);
-                Mp.w1v = mlp_row_elem(S, v, dst);
-                pre = true;
-            }
-        }
-        // (table policy: the action table's entry goes out with the gather, not after it)
-        int tab = 0;
-        if constexpr (!MLPK) {
-            if (fused && dst != v) tab = table_action(S, v * (uint32_t)L.N() + dst);
-        }
-        const uint32_t obs_links = observe_links(S, R, H, v, ns_to_sec(H.now));
-        double reward = 0.0;
-        int32_t prev = -1;
-        uint32_t start, uid, last = 0u;
-        if (fresh) {
-            // first notification: destination from the flow, uid and start second rebuilt from
-            // their low bits (the packet left its app less than 1 s and fewer than 2^20
-            // injections ago)
-            const uint32_t s0 = (uint32_t)(TSEC(H.now));
-            start = s0 - ((s0 ^ f_parity(x)) & 1u);
-            const uint32_t lu = H.uid - 1u;
-            uid = lu - ((lu - f_uid(x)) & kUidMask);
-        } else {
-            // the previous decision (the temp_obs entry of forwarder.py:153-159) from the aux
-            // words: its time less than 2^32 ns ago (a FIFO and a wire crossing)
-            prev = (int32_t)(d - dist);
-            if (dist >= L.log_cap()) fail(H, PRISMA_EBIT_LOGWRAP);
-            uid = a1;
-            start = a2 >> 16;
-            last = a2 & 255u;
-            const int64_t t_prev = H.now - (int64_t)(uint32_t)(lo32(H.now) - a0);
-            reward = (double)py_micros(H.now) / 1e6 - (double)py_micros(t_prev) / 1e6;   // forwarder.py:360
-            CNT_ADD(S, reward_sum, reward);
-        }
-        wire_pop(S, R, H, l, k);
-        H.dec = d + 1u;
-        // obs[0] = m_map_overlay_array[dst] (the identity on identity overlays)
-        const uint32_t o = (lane == 0) ? dst : obs_links;
-        CNT_ADD(S, decisions, 1u);
-        // --train: the answer to this notification also echoes a small-signalling packet to
-        // the last hop, unless this node is the packet's source (:303-306)
-        const uint32_t echo = (S.ctrl && L.train() && v != ent_src(x, v)) ? PEND_ECHO : 0u;
-        D.x = x; D.dst = dst; D.start = start; D.uid = uid; D.v = v; D.d = d; D.reward = reward; D.prev = prev;
-        D.obs = o; D.flags = echo; D.last = last; D.ttl = 255u;        // SetIpTtl(255) (poisson-application.cc:330)
-        D.tab = tab;
-        if (dst == v) {                                             // getGameOver
-            write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_DESTINATION, o, 255u);
-            if (!fused && S.ctrl && L.notify_dest()) {              // the agent is notified (done=True)
-                D.flags |= PEND_DEST;
-                return 1;
-            }
-            if (echo) send_echo(S, R, H, (uint32_t)t_lrev(S, l), uid, last);
-            receive_counters(S, R, H, x, true, start, 0u);
-            return 0;
-        }
-        if (!fused) write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_PENDING, o, 255u);
-        return 1;
-    }
-    wire_pop(S, R, H, l, k);
-    if (S.ctrl && ent_is_big(x)) {                                  // (only with --signaling and --train)
-        const uint32_t bp = t_bpair(S, g_gen(x));
-        const uint32_t src = bp_src(bp);
-        if (v == src) {                  // from the traffic node: IP-forwarded towards its destination
-            if (!link_send(S, R, H, bp_link(bp), x)) CNT_ADD(S, ctrl_dropped, 1u);
-            return 0;
-        }
-        // BigSignalingPacketManager::receivePacket (big-signaling-packet-manager.cc:93-108)
-        if (!fused && L.notify_dest()) {
-            const uint32_t n = g_n(x), ns = t_bs_nseg(S);
-            const uint32_t nn = ns <= 1u ? n : n / ns, seg = ns <= 1u ? 0u : n % ns;
-            const uint32_t so = 0x10000u | src;
-            D.x = x; D.v = v; D.uid = 0u; D.flags = PEND_CTRL; D.last = 0u;
-            D.obs = (lane == 0) ? 1000u : ((lane == 1) ? nn : ((lane == 2) ? seg : ((lane == 3) ? so : 0u)));
-            return 1;
-        }
-        receive_counters(S, R, H, x, false, 0u, l);
-        return 0;
-    }
-    if (S.ctrl && ent_is_echo(x)) {                                 // (echoes exist only with --train)
-        // SmallSignalingPacketManager::receivePacket (small-signaling-packet-manager.cc:86-94)
-        if (!fused && L.notify_dest()) {
-            D.x = x; D.v = v; D.uid = e_uid(x); D.flags = PEND_CTRL; D.last = 0u;
-            const uint32_t sz = ent_size(S, x, l);
-            D.obs = (lane == 0) ? 1000u : ((lane == 1) ? e_uid(x) : ((lane == 2) ? sz : 0u));
-            return 1;
-        }
-        receive_counters(S, R, H, x, false, 0u, l);
-        return 0;
-    }
-    // pings (identity overlays: tunnel == link, every node an overlay node; a ping-forward on
-    // link t arrives over t itself, the ping-back for tunnel t over the reverse of t)
-    const uint32_t t = p_tunnel(x), rnd = p_round(x);
-    if (type == T_PFWD) {                                           // ping-forward-packet-manager.cc:94-156
-        const float delay = (float)(ns_to_sec(H.now) - ping_send_s(L, rnd));
-        st_rep(S, &S.pbd[t * L.PBK() + (rnd & (L.PBK() - 1))], delay);
-        if (!link_send(S, R, H, (uint32_t)t_lrev(S, l), p_make(T_PBACK, t, 0u, rnd))) CNT_ADD(S, ctrl_dropped, 1u);
-    } else {                                                        // ping-back-packet-manager.cc:120-144
-        const float delay = __uint_as_float(u_ld32((const uint32_t*)S.pbd + t * L.PBK() + (rnd & (L.PBK() - 1))));
-        ping_ack(S, R, H, t, rnd, delay);
-    }
-    receive_counters(S, R, H, x, false, 0u, l);
-    return 0;
-}
-
-// ---------------------------------------------------------------------------
 // binding, init, staging
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void mem_bind(Sim& S, MemSt& R, const KParams& P, const LV& lv, unsigned char* lds, int r,
@@ -540,8 +389,6 @@ __device__ __forceinline__ void mem_bind(Sim& S, MemSt& R, const KParams& P, con
     R.n2 = LC.n2;
     R.RW = LC.lrec_words;
     R.WCAP = (uint32_t)LC.WCAP;
-    R.laux = (uint32_t*)(img + LC.g_laux);
-    R.AW = 4u * (uint32_t)LC.WCAP;
     R.fblk = make_uint4(0u, 0u, 0u, 0u);
     R.fblk_b = ~0u;
 }
@@ -699,8 +546,8 @@ extern "C" int prisma_debug_trace(void* dev_buf, unsigned int cap) {
 // diagnostic build only: read and clear the memory-resident engine's per-phase cycle totals
 extern "C" int prisma_debug_timing_mem(unsigned long long* out16) {
     if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prisma_timing), 48 * sizeof(unsigned long long)) != hipSuccess) return -1;
-    unsigned long long z[48] = {0};
+        hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prisma_timing), 32 * sizeof(unsigned long long)) != hipSuccess) return -1;
+    unsigned long long z[32] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif
