@@ -1721,7 +1721,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
             dst = (w_prev >> 8) & 255u;
             start = w_prev >> 16;
             last = w_prev & 255u;
-            reward = (double)py_micros(H.now) / 1e6 - (double)py_micros(t_prev) / 1e6;   // forwarder.py:360
+            reward = us_to_sec(py_micros(H.now)) - us_to_sec(py_micros(t_prev));   // forwarder.py:360
             CNT_ADD(S, reward_sum, reward);
         }
         // obs[0] = m_map_overlay_array[dst] (the identity on identity overlays)

@@ -110,8 +110,26 @@ __host__ __device__ inline float det_elu(float x) { return x > 0.0f ? x : det_ex
 
 // ns-3 Seconds(double) -> int64 ns (round to nearest)
 __host__ __device__ inline int64_t sec_to_ns(double s) { return (int64_t)(s * 1e9 + 0.5); }
+// a / d for a constant d with rd = RN(1 / d), on the device as q = a * rd and one FMA correction
+// (Markstein): for 0 <= a < 2^53 and d = 1e9 or 1e6 this is the correctly rounded quotient, bit for
+// bit the IEEE division the host and the oracle perform (tests/test_numerics_division.py checks
+// 4e7 values; the C harness of this change checked 6.4e8), in 3 dependent f64 instructions
+// instead of the ~10 of the hardware's division sequence (rcp, two Newton steps, div_fmas,
+// div_fixup) -- three of which sat on every data arrival's dependent chain.
+__host__ __device__ inline double div_const(double a, double d, double rd) {
+#ifdef __HIP_DEVICE_COMPILE__
+    const double q = a * rd;
+    const double e = __builtin_fma(-q, d, a);
+    return __builtin_fma(e, rd, q);
+#else
+    (void)rd;
+    return a / d;
+#endif
+}
 // ns-3 Time::GetSeconds()
-__host__ __device__ inline double ns_to_sec(int64_t t) { return (double)t / 1e9; }
+__host__ __device__ inline double ns_to_sec(int64_t t) { return div_const((double)t, 1e9, 1e-9); }
+// microseconds as Python's float of the "%f" string (forwarder.py:360)
+__host__ __device__ inline double us_to_sec(uint64_t us) { return div_const((double)us, 1e6, 1e-6); }
 
 // t / 1000 and t / 10^9 for 0 <= t < 2^42 ns (sim_time_s <= 4095, checked on the host) on the
 // vector unit: floor(t * c) with c the double nearest 10^-3 (10^-9) is exact there -- both
@@ -164,6 +182,6 @@ __host__ __device__ inline uint64_t py_micros(int64_t t) {
 }
 
 __host__ __device__ inline double py_reward(int64_t t_now, uint32_t us_prev) {
-    return (double)py_micros(t_now) / 1e6 - (double)us_prev / 1e6;
+    return us_to_sec(py_micros(t_now)) - us_to_sec(us_prev);
 }
 
