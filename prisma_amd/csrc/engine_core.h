@@ -666,18 +666,27 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
     // (--train instances: an echo's by link, sized by its sender)
     // (memory-resident: by entry type from the scenario constants; --train instances: echoes by
     // link, big-signalling segments from the BigSig header)
-    int64_t tx = sw ? (S.mem ? ((S.ctrl && ent_is_echo(x)) ? (int64_t)t_etx(S, l)
-                                : ((S.ctrl && ent_is_big(x)) ? (int64_t)S.m_bs->tx_sw
-                                   : (ent_is_data(x) ? L.sw_txd() : (ent_is_echo(x) ? L.sw_txe() : L.sw_txp()))))
-                             : (int64_t)((S.ctrl && ent_is_echo(x)) ? S.T->etx[l] : S.T->ctx[ent_cls(x)]))
-                    : ((S.ctrl && ent_is_big(x)) ? (int64_t)t_abtx(S, l - (uint32_t)L.E())
-                                                 : t_acctx(S, l - (uint32_t)L.E()));
-    int64_t prop = sw ? L.sw_prop() : 0;
+    uint32_t at;
     k.busy = 1;
-    k.cp_t = lo32(H.now + tx);
+    if (S.mem) {
+        int64_t tx = sw ? ((S.ctrl && ent_is_echo(x)) ? (int64_t)t_etx(S, l)
+                           : ((S.ctrl && ent_is_big(x)) ? (int64_t)S.m_bs->tx_sw
+                              : (ent_is_data(x) ? L.sw_txd() : (ent_is_echo(x) ? L.sw_txe() : L.sw_txp()))))
+                        : ((S.ctrl && ent_is_big(x)) ? (int64_t)t_abtx(S, l - (uint32_t)L.E())
+                                                     : t_acctx(S, l - (uint32_t)L.E()));
+        int64_t prop = sw ? L.sw_prop() : 0;
+        k.cp_t = lo32(H.now + tx);
+        at = lo32(H.now + tx + prop);
+    } else {
+        // register-resident engine: (tx, tx + propagation) of link l for the entry's class, low 32
+        // bits, one scalar load from the topology image (TopoImage::ltx) -- the switch/access
+        // selects, the 64-bit adds and the second load are the host's
+        const uint32_t i = 2u * (l * 8u + ent_cls(x));
+        k.cp_t = lo32(H.now) + S.T->ltx[i];
+        at = lo32(H.now) + S.T->ltx[i + 1u];
+    }
     k.cp_seq = H.seq++;                                        // TransmitComplete
     const uint32_t w = ring_idx & (uint32_t)(L.WCAP() - 1);
-    const uint32_t at = lo32(H.now + tx + prop);
     const uint32_t as = H.seq++;                               // channel Receive
     wire_set(S, k, l, w, at, as, x);
     if (k.n_wire == 1) { k.wh_t = at; k.wh_seq = as; }        // the wire was empty: new head
@@ -724,14 +733,19 @@ __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l
     const LV& L = S.lv;
     LinkV k = link_get(R, l);
     uint32_t size = ent_size(S, e, l);
-    bool ok = l < (uint32_t)L.E() ? (k.qb + size <= L.qmax_bytes()) : (k.n_queue + 1u <= L.acc_qmax_pkts());
-    if (!ok) return 0;
+    // admission (switch links by queued bytes, access links by queued packets) as one compare
+    // of selected operands: the compiler had branched on the link kind
+    const bool sw = l < (uint32_t)L.E();
+    const uint32_t have = sw ? k.qb + size : k.n_queue + 1u;
+    const uint32_t lim = sw ? L.qmax_bytes() : L.acc_qmax_pkts();
+    if (have > lim) return 0;
     if (RS::kLazy) {
         // the transmitter's completion was elided (nothing queued behind it): if it precedes
-        // the event being executed it has happened -- count it now (lazy_due)
-        const bool due = k.busy && k.n_queue == 0u && lazy_due(k.n_wire, k.cp_t, k.cp_seq, H);
-        k.busy = due ? 0u : k.busy;
-        H.ev_launch += due ? 1u : 0u;
+        // the event being executed it has happened -- count it now (lazy_due).  A uniform branch
+        // on the elided state: the combined condition had become ~15 scalar mask operations
+        if (k.busy && k.n_queue == 0u) {
+            if (lazy_due(k.n_wire, k.cp_t, k.cp_seq, H)) { k.busy = 0u; H.ev_launch++; }
+        }
     }
     uint32_t cap = ring_cap(S, l), off = ring_off(S, l);
     if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
@@ -1232,6 +1246,21 @@ __device__ __forceinline__ void mlp_preload(MlpPre& M, const float* __restrict__
     M.b4 = RP[2 * mlp_rp_layer_floats(64) + 64 * D + l4];
 }
 
+// mlp_preload's layer-3 and layer-4 halves (the memory-resident engine issues them apart)
+__device__ __forceinline__ void mlp_preload_w3(MlpPre& M, const float* __restrict__ RP, int lane) {
+    const float4* __restrict__ W3 = (const float4*)(RP + mlp_rp_layer_floats(64));
+#pragma unroll
+    for (int c = 0; c < 16; ++c) M.w3[c] = W3[c * 64 + lane];
+    M.b3 = RP[mlp_rp_layer_floats(64) + 64 * 64 + lane];
+}
+__device__ __forceinline__ void mlp_preload_w4(MlpPre& M, const float* __restrict__ RP, int lane, int D, int deg) {
+    const float4* __restrict__ W4 = (const float4*)(RP + 2 * mlp_rp_layer_floats(64));
+    const int l4 = lane < deg ? lane : 0;
+#pragma unroll
+    for (int c = 0; c < 16; ++c) M.w4[c] = W4[c * D + l4];
+    M.b4 = RP[2 * mlp_rp_layer_floats(64) + 64 * D + l4];
+}
+
 // layers 1-2 of a decision at node v (the one-hot row too when the destination dst is
 // known, has_w1): issued by the memory-resident engine's arrival handler together with
 // its second round trip (previous decision record, observation), so the decision finds
@@ -1430,7 +1459,10 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
         __builtin_amdgcn_sched_barrier(0);
     }
     MlpPre M;
-    if constexpr (B == kMlpAll) mlp_preload(M, RP, lane, D, deg, !PRE);   // PRE: layer 2 came with the arrival
+    // PRE (memory-resident engine): layer 2 came with the arrival, and layers 3-4 are issued in
+    // two halves inside the LayerNorm below, so their issue overlaps its dependent chain instead
+    // of holding the wave in front of it
+    if constexpr (B == kMlpAll && !PRE) mlp_preload(M, RP, lane, D, deg, true);
     float b1v;
     float4 wb[4];
     if constexpr (PRE) {
@@ -1456,12 +1488,22 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     float sum = 0.0f;
     if constexpr (B == kMlpAll) sum = lane_sum_ordered(xf, deg);
     else for (int k = 0; k < deg; ++k) sum = __fadd_rn(sum, rdlf(xf, (uint32_t)(k + 1)));
+    if constexpr (B == kMlpAll && PRE) {
+        __builtin_amdgcn_sched_barrier(0);
+        mlp_preload_w3(M, RP, lane);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     const float mean = __fdiv_rn(sum, (float)deg);
     const float dv = __fsub_rn(xf, mean);
     const float sq = __fmul_rn(dv, dv);
     float var = 0.0f;
     if constexpr (B == kMlpAll) var = lane_sum_ordered(sq, deg);
     else for (int k = 0; k < deg; ++k) var = __fadd_rn(var, rdlf(sq, (uint32_t)(k + 1)));
+    if constexpr (B == kMlpAll && PRE) {
+        __builtin_amdgcn_sched_barrier(0);
+        mlp_preload_w4(M, RP, lane, D, deg);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     var = __fdiv_rn(var, (float)deg);
     const float den = __fsqrt_rn(__fadd_rn(var, 1e-3f));
     const float xn = __fdiv_rn(dv, den);                          // lane k+1: normalised value k

@@ -133,6 +133,9 @@ struct TopoImage {
                                  // position mask << 16 (overlay nodes on the tunnel, target included)
     uint32_t ctx[8];             // transmission time on a switch link of an entry of class
                                  // (type | echo bit << 2), ns (< 2^31)
+    uint32_t ltx[256 * 8 * 2];   // link l, entry class c: (tx, tx + propagation), ns, low 32 bits --
+                                 // ctx / acctx / etx / abtx and the switch links' propagation
+                                 // delay folded per link (engine_core.h transmit_start)
     // signalling (read only by the --train instances, step_kernel.h CTRL)
     uint32_t esz[256];           // switch link l: size of an echo crossing it (its sender's payload
                                  // + 30 B: one hop on identity overlays, uniform on tunnelled ones)

@@ -870,6 +870,15 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     memcpy(TI.esz, SG.esz.data(), 4u * E);
     memcpy(TI.etx, SG.etx.data(), 4u * E);
     memcpy(TI.abtx, SG.abtx.data(), 4u * N);
+    for (int l = 0; l < Lk; ++l)                     // (tx, tx + prop) by link and entry class
+        for (uint32_t c = 0; c < 8; ++c) {
+            const bool sw = l < E;
+            const int64_t tx = sw ? (c == 7u ? (int64_t)SG.etx[l] : (int64_t)TI.ctx[c])
+                                  : (c == 6u ? (int64_t)SG.abtx[l - E] : acctx[l - E]);
+            const int64_t prop = sw ? L.sw_prop : 0;
+            TI.ltx[2 * (l * 8 + (int)c)] = (uint32_t)tx;
+            TI.ltx[2 * (l * 8 + (int)c) + 1] = (uint32_t)(tx + prop);
+        }
     for (int g = 0; g < G; ++g) TI.bpair[g] = bpair[g];
     for (int f = 0; f < F; ++f) TI.fseq[f] = SG.fseq[f];
     if (G) TI.fseq[F] = SG.fseq[F];
