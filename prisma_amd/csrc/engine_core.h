@@ -536,8 +536,11 @@ __device__ __forceinline__ uint32_t wave_umin_fast(uint32_t v);
 // so the completion lies within one propagation delay before the clock or one transmission
 // after it (< 2^31 ns, checked on the host) and its 32-bit time offset is exact.
 __device__ __forceinline__ bool lazy_due(uint32_t n_wire, uint32_t cp_t, uint32_t cp_seq, const Hot& H) {
-    const int32_t dt = (int32_t)(cp_t - lo32(H.now));
-    return n_wire == 0u || dt < 0 || (dt == 0 && cp_seq < H.cur_seq);
+    // (dt, cp_seq) < (0, cur_seq) with dt = cp_t - lo32(now) as a signed 32-bit offset: the sign
+    // of dt * 2^32 + cp_seq - cur_seq, one 64-bit subtraction (|dt| < 2^31 whenever the wire holds
+    // a packet, so the difference does not wrap; with an empty wire it is not consulted)
+    const uint64_t d = ((uint64_t)(cp_t - lo32(H.now)) << 32) + (uint64_t)cp_seq - (uint64_t)H.cur_seq;
+    return n_wire == 0u || (int64_t)d < 0;
 }
 
 // Settle every elided completion that precedes the current event, or -- at the end of an
@@ -743,7 +746,9 @@ __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l
         // the transmitter's completion was elided (nothing queued behind it): if it precedes
         // the event being executed it has happened -- count it now (lazy_due).  A uniform branch
         // on the elided state: the combined condition had become ~15 scalar mask operations
-        if (k.busy && k.n_queue == 0u) {
+        // (busy is 0 or 1: one compare of the packed transmitter word instead of two conditions
+        // the compiler combined as 64-bit lane masks)
+        if (((k.busy << 16) | k.n_queue) == 0x10000u) {
             if (lazy_due(k.n_wire, k.cp_t, k.cp_seq, H)) { k.busy = 0u; H.ev_launch++; }
         }
     }
@@ -956,7 +961,7 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
     v = rfl(v);                                     // (scalar loads of the row pointers)
     int r0 = t_ovrow(S, v), deg = t_ovrow(S, v + 1) - r0;
     uint32_t status;
-    if (action >= 0 && action < deg) {
+    if ((uint32_t)action < (uint32_t)deg) {                      // 0 <= action < deg
         const uint32_t l = tunnel_link(S, (uint32_t)(r0 + action));   // RouteOutput (:281-287)
         CNT_ADD(S, hops, 1u);
         CNT_ADD(S, hop_deg_sum, (uint64_t)deg);
