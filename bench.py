@@ -9,7 +9,7 @@ forward pass over every (node, dst)) + one engine launch in which every
 replica executes `--hops` forwarding decisions (enqueue or drop), logging
 one decision record per data notification to HBM.
 
-Run: python bench.py [--gpus N --steps K --warmup W].  N > 1: one process per
+Run: python bench.py [--gpus N --steps K --warmup W] [--preset configK].  N > 1: one process per
 GPU over RCCL, either under torch.distributed.run (RANK/WORLD_SIZE set) or
 launched by this script itself (it starts N child ranks before anything
 touches the GPU, then waits for them).  Replicas are sharded (weak scaling:
@@ -17,6 +17,11 @@ replica ids rank*R .. rank*R+R-1), no data-path collective; the per-replica
 episode statistics are all-gathered over RCCL at the end.  --same-device runs
 the N ranks on cuda:0 over gloo (a rehearsal of the spawn/gather/JSON path on
 a one-GPU box; its value is not a scaling figure).
+
+--preset config1 ... config5 selects one BASELINE.json configuration per GPU (replicas per GPU
+fixed, weak scaling: config 4's 16 384 GEANT replicas and config 5's 8 192 ER-256 replicas are
+2 048 and 1 024 per GPU at N = 8), config4 with its load-factor sweep: one JSON line per load
+factor (--load-factors overrides the sweep).  Explicit flags override a preset's values.
 """
 from __future__ import annotations
 
@@ -38,26 +43,45 @@ METRIC = "packet-hop transitions/sec at 4096 Abilene replicas; achieved HBM GB/s
 HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
 
-def parse():
+# BASELINE.json configs, per GPU (weak scaling): explicit flags override these values
+PRESETS = {
+    "config1": dict(topology="abilene", policy="sp", replicas=1, ping_as_obs=1, hops=2048),
+    "config2": dict(topology="abilene", policy="dq_routing", replicas=4096, ping_as_obs=1),
+    "config3": dict(topology="abilene_on_geant", policy="dqn_buffer", replicas=4096, ping_as_obs=1),
+    "config4": dict(topology="geant", policy="dqn_buffer", replicas=2048, ping_as_obs=0,
+                    load_factors="0.5,0.75,1.0,1.25,1.5,1.75,2.0"),
+    "config5": dict(topology="er256", policy="dqn_buffer", replicas=1024, ping_as_obs=1),
+}
+DEFAULTS = dict(topology="abilene", policy="dq_routing", ping_as_obs=1, hops=8192, load_factor=1.0)
+
+
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--preset", choices=sorted(PRESETS), default=None,
+                   help="a BASELINE.json configuration (per GPU); explicit flags override its values")
+    p.add_argument("--load-factors", default=None,
+                   help="comma-separated load factors: one measurement and JSON line each (config 4's sweep)")
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=None,
                    help="untimed steps (default 2; er256: past the first simulated second, whose 65 251 "
                         "flow-start events are a transient of the episode)")
     p.add_argument("--replicas", type=int, default=None, help="replicas per GPU (default 4096; er256: 1024 = "
                                                              "BASELINE config 5's 8192 over 8 GPUs)")
-    p.add_argument("--hops", type=int, default=8192, help="hops per replica per step (default 8192: one launch "
+    p.add_argument("--hops", type=int, default=None, help="hops per replica per step (default 8192: one launch "
                    "of ~60 ms at the headline, so the per-step policy refresh and launch costs stay ~1 %%)")
-    p.add_argument("--topology", default="abilene")
+    p.add_argument("--topology", default=None)
     p.add_argument("--tm", type=int, default=0)
-    p.add_argument("--load-factor", type=float, default=1.0)
-    p.add_argument("--ping-as-obs", type=int, default=1)
-    p.add_argument("--policy", default="dq_routing", choices=["dq_routing", "dqn_buffer", "sp"],
+    p.add_argument("--load-factor", type=float, default=None)
+    p.add_argument("--ping-as-obs", type=int, default=None)
+    p.add_argument("--policy", default=None, choices=["dq_routing", "dqn_buffer", "sp"],
                    help="in-kernel policy: DQ-routing argmin table (BASELINE configs[1]), DQN-buffer MLP, SP table")
     p.add_argument("--cpu-baseline", type=int, default=1)
-    p.add_argument("--cpu-hops", type=int, default=8000000, help="oracle hops per host thread (cpu_baseline)")
-    p.add_argument("--cpu-hops-1core", type=int, default=4000000, help="oracle hops of the single-thread pass")
+    p.add_argument("--cpu-hops", type=int, default=None,
+                   help="oracle hops per host thread (cpu_baseline; default 8e6 with a table policy, 1.2e6 with "
+                        "the DQN-buffer MLP: ~10-20 s of host work either way)")
+    p.add_argument("--cpu-hops-1core", type=int, default=None, help="oracle hops of the single-thread pass "
+                   "(default: half of --cpu-hops)")
     p.add_argument("--same-device", action="store_true",
                    help="N ranks share cuda:0 over gloo (rehearsal of the N-rank path on one GPU)")
     p.add_argument("--rank-deadline", type=float, default=None,
@@ -72,12 +96,25 @@ def parse():
                         "RCCL init and the all-gather on a one-GPU box)")
     p.add_argument("--backend", default=None, choices=["nccl", "gloo"],
                    help="process-group backend (default: nccl = RCCL; gloo with --same-device)")
-    a = p.parse_args()
+    a = p.parse_args(argv)
+    for k, v in (PRESETS[a.preset] if a.preset else {}).items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    for k, v in DEFAULTS.items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
     big = a.topology == "er256"
     if a.replicas is None:
         a.replicas = 1024 if big else 4096
     if a.warmup is None:
         a.warmup = 13 if big else 2          # er256: 13 x 8192 hops ~ 1.3 simulated seconds
+    a.lfs = ([float(x) for x in a.load_factors.split(",") if x.strip()] if a.load_factors
+             else [float(a.load_factor)])
+    mlp = a.policy == "dqn_buffer"
+    if a.cpu_hops is None:
+        a.cpu_hops = 1200000 if mlp else 8000000
+    if a.cpu_hops_1core is None:
+        a.cpu_hops_1core = a.cpu_hops // 2
     return a
 
 
@@ -114,45 +151,75 @@ def host_cpus():
     return use, {"nproc": nproc, "affinity": aff, "cgroup_quota_cpus": quota, "model": model}
 
 
-def cpu_baseline(topo, params, table, hops_per_thread: int, hops_1core: int):
+def cpu_baseline(topo, params, kind: str, policy, hops_per_thread: int, hops_1core: int, threads: int = None,
+                 warm_hops: int = 0, workload: str = ""):
     """The C oracle (oracle/, kind 'port') on the host: one replica per thread over every CPU this
-    job may use (each thread runs back-to-back episodes, as auto-reset does, until it executed
-    `hops_per_thread` hops), and a single-thread pass for the per-core figure."""
+    job may use (at most `threads`: config 1 has one replica), each running back-to-back episodes,
+    as auto-reset does, until it executed `hops_per_thread` hops, and a single-thread pass for the
+    per-core figure.  kind "table": the [N, N] action table (SP / DQ-routing); "mlp": the packed
+    DQN-buffer weights, decided by the oracle's fixed-order fp32 restatement of the in-kernel MLP
+    (models.py:258-306).  warm_hops: executed untimed first on every thread (the GPU line's warm-up
+    past ER-256's flow-start transient)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     O.build()
-    cores, host = host_cpus()
+    avail, host = host_cpus()
+    cores = avail if threads is None else max(1, min(avail, int(threads)))
+    pol = np.ascontiguousarray(policy)
 
     def timed(n_threads, hops_each):
         done = [0] * n_threads
         episodes = [0] * n_threads
+        sims = [None] * n_threads
+        bar = threading.Barrier(n_threads + 1)
+
+        def run(sim, n):
+            return sim.run_table(pol, n) if kind == "table" else sim.run_mlp(pol, n)
 
         def work(i):
             ep = 0
+            sims[i] = O.OracleSim(topo, params, replica=100000 + i, episode=ep)
+            w = 0
+            while w < warm_hops:                    # untimed (ends inside the first episode here)
+                got = run(sims[i], warm_hops - w)
+                w += got
+                if w < warm_hops:
+                    ep += 1
+                    sims[i].close()
+                    sims[i] = O.OracleSim(topo, params, replica=100000 + i, episode=ep)
+            bar.wait()
             while done[i] < hops_each:
-                sim = O.OracleSim(topo, params, replica=100000 + i, episode=ep)
-                done[i] += sim.run_table(table, hops_each - done[i])   # ctypes releases the GIL
-                sim.close()
-                ep += 1
-            episodes[i] = ep
+                done[i] += run(sims[i], hops_each - done[i])   # ctypes releases the GIL
+                if done[i] < hops_each:
+                    sims[i].close()
+                    ep += 1
+                    sims[i] = O.OracleSim(topo, params, replica=100000 + i, episode=ep)
+            sims[i].close()
+            episodes[i] = ep + 1
+            bar.wait()
 
         ths = [threading.Thread(target=work, args=(i,)) for i in range(n_threads)]
-        t0 = time.perf_counter()
         for t in ths:
             t.start()
+        bar.wait()                                  # every thread built (and warmed) its replica
+        t0 = time.perf_counter()
+        bar.wait()
+        dt = time.perf_counter() - t0
         for t in ths:
             t.join()
-        dt = time.perf_counter() - t0
         return int(sum(done)), int(sum(episodes)), dt
 
     h1, e1, d1 = timed(1, hops_1core)
     hn, en, dn = timed(cores, hops_per_thread)
+    what = "DQN-buffer MLP (the oracle's fixed-order fp32 restatement)" if kind == "mlp" else "action table"
+    warm = f", each thread first {warm_hops} hops untimed" if warm_hops else ""
     return {"value": hn / dn, "unit": "hops/s", "cores": cores, "kind": "port",
-            "value_1core": h1 / d1, "host": host,
-            "sample": f"{cores} host threads x {hops_per_thread} hops ({en} Abilene episodes of "
-                      f"{params['sim_time_s']:g} s, same params and DQ-routing table), {hn} hops in {dn:.1f} s wall; "
+            "value_1core": h1 / d1, "host": host, "workload": workload,
+            "sample": f"{cores} host threads x {hops_per_thread} hops ({en} {topo.name} episodes of "
+                      f"{params['sim_time_s']:g} s, same params and {what}{warm}), {hn} hops in {dn:.1f} s wall; "
                       f"1 thread x {hops_1core} hops in {d1:.1f} s; {cores} = the CPUs this job may use "
-                      f"(affinity {host['affinity']}, cgroup quota {host['cgroup_quota_cpus']}, nproc {host['nproc']}); "
+                      f"(affinity {host['affinity']}, cgroup quota {host['cgroup_quota_cpus']}, nproc {host['nproc']})"
+                      f"{', capped at the replica count' if cores < avail else ''}; "
                       f"the ns-3 reference path is not runnable here (SURVEY 8c)"}
 
 
@@ -199,7 +266,7 @@ RANK_STAGES = ("started", "init", "timed", "done")
 def rank_deadline(args) -> float:
     if args.rank_deadline is not None:
         return float(args.rank_deadline)
-    return INIT_ALLOWANCE_S + STEP_BOUND_S * (args.warmup + args.steps) + CPU_BASELINE_ALLOWANCE_S
+    return INIT_ALLOWANCE_S + (STEP_BOUND_S * (args.warmup + args.steps) + CPU_BASELINE_ALLOWANCE_S) * len(args.lfs)
 
 
 def report_stage(stage: str) -> None:
@@ -300,7 +367,10 @@ def rendezvous_only(args, world: int, rank: int) -> None:
     report_stage("timed")
     if rank == 0:
         print(json.dumps({"rendezvous": "ok", "backend": backend, "world_size": dist.get_world_size(),
-                          "replicas_gathered": int(t.sum().item()), "per_rank_replicas": t.cpu().tolist()}),
+                          "replicas_gathered": int(t.sum().item()), "per_rank_replicas": t.cpu().tolist(),
+                          "workload": {"preset": args.preset, "topology": args.topology, "policy": args.policy,
+                                       "replicas_per_gpu": args.replicas, "ping_as_obs": args.ping_as_obs,
+                                       "load_factors": args.lfs, "hops": args.hops, "warmup": args.warmup}}),
               flush=True)
     dist.destroy_process_group()
     report_stage("done")
@@ -343,13 +413,25 @@ def main():
     report_stage("init")
     coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
+    for lf in args.lfs:
+        measure(args, lf, world, rank, use_dist, backend, coll_dev, dev, local)
+    if use_dist:
+        dist.destroy_process_group()
+    report_stage("done")
+
+
+def measure(args, lf, world, rank, use_dist, backend, coll_dev, dev, local):
+    """One workload (the arguments at load factor lf): W untimed steps, K timed steps bracketed by a
+    barrier and device synchronisation, the max over ranks; rank 0 prints its JSON line."""
+    import torch
+    import torch.distributed as dist
     from prisma_amd.config import engine_params
     from prisma_amd.dist import gather_replica_stats, shard
     from prisma_amd.engine import PrismaEngine, build_id
     from prisma_amd.policies import StackedQNet
     from prisma_amd.topology import Topology, sp_next_hop_table
 
-    topo = Topology.example(args.topology, args.tm, args.load_factor)
+    topo = Topology.example(args.topology, args.tm, lf)
     base, R = shard(args.replicas * world, rank, world)
     # the decision log must outlive one link crossing (queueing included): ER-256 makes
     # ~80 k decisions per simulated second against up to ~0.27 s per crossing
@@ -425,6 +507,8 @@ def main():
         traffic = pmc_traffic(args.topology, args.replicas, args.hops, bid)
         metric = METRIC if (args.topology, args.replicas) == ("abilene", 4096) else \
             f"packet-hop transitions/sec at {args.replicas} {topo.name} replicas; achieved HBM GB/s"
+        workload = (f"{args.topology} tm{args.tm} lf{lf} {args.policy} greedy, {args.replicas} replicas/GPU x "
+                    f"{args.hops} hops/step, pingAsObs={args.ping_as_obs}, simTime 60 s auto-reset")
         result = {
             "metric": metric,
             "value": hops_total / elapsed,
@@ -438,11 +522,9 @@ def main():
             "vs_baseline": None,
             "dtype": "int64",
             "data": f"synthetic (Poisson traffic from the shipped {topo.name} TM{args.tm} x load_factor "
-                    f"{args.load_factor}; {'random-init ' + args.policy + ' weights' if args.policy != 'sp' else 'SP table'})",
+                    f"{lf}; {'random-init ' + args.policy + ' weights' if args.policy != 'sp' else 'SP table'})",
             "config": {
-                "workload": f"{args.topology} tm{args.tm} lf{args.load_factor} {args.policy} greedy, "
-                            f"{args.replicas} replicas/GPU x {args.hops} hops/step, pingAsObs={args.ping_as_obs}, "
-                            f"simTime 60 s auto-reset",
+                "workload": workload, "preset": args.preset, "load_factor": lf,
                 "topology": args.topology, "replicas_per_gpu": args.replicas, "hops_per_step": args.hops,
                 "policy": args.policy, "parallelism": f"replica-sharded x{world}"
                 + (" (ranks share cuda:0 over gloo: rehearsal, not a scaling figure)" if args.same_device else ""),
@@ -464,14 +546,15 @@ def main():
             "replicas_total": int(stats["stats"].shape[0]),
             "per_rank_hops_s": [h / elapsed for h in per_rank],
         }
-        if args.cpu_baseline and world == 1 and args.policy != "dqn_buffer":
-            result["cpu_baseline"] = cpu_baseline(topo, dict(params, auto_reset=0),
-                                                  policy().cpu().numpy(), args.cpu_hops, args.cpu_hops_1core)
+        if args.cpu_baseline and world == 1:
+            kind = "mlp" if args.policy == "dqn_buffer" else "table"
+            # warm-up equal to the GPU line's (hops per replica before the timed steps)
+            warm = args.warmup * args.hops if args.topology == "er256" else 0
+            result["cpu_baseline"] = cpu_baseline(topo, dict(params, auto_reset=0), kind, policy().cpu().numpy(),
+                                                  args.cpu_hops, args.cpu_hops_1core, threads=args.replicas,
+                                                  warm_hops=warm, workload=workload)
         print(json.dumps(result), flush=True)
     eng.close()
-    if use_dist:
-        dist.destroy_process_group()
-    report_stage("done")
 
 
 if __name__ == "__main__":

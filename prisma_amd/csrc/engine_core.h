@@ -50,11 +50,20 @@ static __device__ unsigned int g_prisma_trace_cap;
 static __device__ unsigned int g_prisma_trace_n[8];
 #endif
 #if PRISMA_TIMING
-static __device__ unsigned long long g_prisma_timing[32];   // one copy per engine (translation unit); 16-19: mlp_action phases
+// one copy per engine (translation unit): 0-7 loop phases, 8-15 their counts, 16-19 mlp_action
+// phases, 20-23 memory-resident on_flow phases, 24-39 fine probes TP(i), 40-55 their counts
+constexpr int kTimingWords = 64;
+static __device__ unsigned long long g_prisma_timing[kTimingWords];
 #define TM_NOW() ((uint64_t)__builtin_amdgcn_s_memtime())
 #define TM_FLOW(i) do { const uint64_t t_ = TM_NOW(); S.tflow[i] += t_ - S.tfl; S.tfl = t_; } while (0)
+// fine probes: cycles since the previous probe (or TP_START) into slot i, scheduling fenced
+#define TP_START() do { __builtin_amdgcn_sched_barrier(0); S.tpl = TM_NOW(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#define TP(i) do { __builtin_amdgcn_sched_barrier(0); const uint64_t t_ = TM_NOW(); S.tp[i] += t_ - S.tpl; S.tpn[i]++; \
+                   S.tpl = t_; __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define TM_FLOW(i) do { } while (0)
+#define TP_START() do { } while (0)
+#define TP(i) do { } while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -322,6 +331,8 @@ struct Sim {
     mutable uint64_t tsub[2], tlast;             // sub-phase cycles inside apply_decision
     mutable uint64_t tmlp[4];                    // mlp_action phases (timing build)
     mutable uint64_t tflow[4], tfl;              // memory-resident on_flow phases (timing build)
+    mutable uint64_t tp[16], tpl;                // fine probes TP(i) (timing build)
+    mutable uint32_t tpn[16];
 #endif
 };
 
@@ -984,12 +995,14 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
 #if PRISMA_TIMING
     { const uint64_t t = TM_NOW(); S.tsub[0] += t - S.tlast; S.tlast = t; }
 #endif
+    TP(12);
     if (fused) write_record(S, H, d, reward, uid, prev, v, dst, start, action, status, obs_reg, ttl);
     else patch_record(S, H, d, action, status);
     receive_counters(S, R, H, x, false, 0u, 0u);
 #if PRISMA_TIMING
     { const uint64_t t = TM_NOW(); S.tsub[1] += t - S.tlast; S.tlast = t; }
 #endif
+    TP(13);
 }
 
 // Answer to the pending notification.  Returns 1 if a hop was executed (0 for a
@@ -1324,6 +1337,9 @@ template <int B, bool EARLY>
 __device__ __forceinline__ float mlp_l234_pipe(const Sim& S, const float* __restrict__ RP, int lane, int D, int deg,
                                                const float4 (&w0)[B]) {
     constexpr int NB = 16 / B, T = 3 * NB;
+    // B must divide the 16 chunks of a layer, and EARLY (issue(0) skipped: the caller issued
+    // batch 0) needs a later batch of layer 2 to load its bias
+    static_assert(16 % B == 0 && (!EARLY || NB >= 2), "mlp_l234_pipe: B must divide 16; EARLY needs 16 / B >= 2");
     const float4* __restrict__ hb = (const float4*)S.hbuf;
     const int l4 = lane < deg ? lane : 0;
     float4 w[2][B];
@@ -1438,6 +1454,11 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
 #else
 #define TM_MLP(i) do { } while (0)
 #endif
+    TP_START();
+#if PRISMA_TIMING
+    if constexpr (PRE) __builtin_amdgcn_s_waitcnt(0);     // the arrival's loads (probe only)
+#endif
+    TP(0);
     const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
     const uint32_t dst = rdl(obs_reg, 0);
     // layer-1 weights first (independent of the normalisation): one W1 row element and
@@ -1493,25 +1514,30 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     float sum = 0.0f;
     if constexpr (B == kMlpAll) sum = lane_sum_ordered(xf, deg);
     else for (int k = 0; k < deg; ++k) sum = __fadd_rn(sum, rdlf(xf, (uint32_t)(k + 1)));
+    TP(1);
     if constexpr (B == kMlpAll && PRE) {
         __builtin_amdgcn_sched_barrier(0);
         mlp_preload_w3(M, RP, lane);
         __builtin_amdgcn_sched_barrier(0);
     }
+    TP(2);
     const float mean = __fdiv_rn(sum, (float)deg);
     const float dv = __fsub_rn(xf, mean);
     const float sq = __fmul_rn(dv, dv);
     float var = 0.0f;
     if constexpr (B == kMlpAll) var = lane_sum_ordered(sq, deg);
     else for (int k = 0; k < deg; ++k) var = __fadd_rn(var, rdlf(sq, (uint32_t)(k + 1)));
+    TP(3);
     if constexpr (B == kMlpAll && PRE) {
         __builtin_amdgcn_sched_barrier(0);
         mlp_preload_w4(M, RP, lane, D, deg);
         __builtin_amdgcn_sched_barrier(0);
     }
+    TP(4);
     var = __fdiv_rn(var, (float)deg);
     const float den = __fsqrt_rn(__fadd_rn(var, 1e-3f));
     const float xn = __fdiv_rn(dv, den);                          // lane k+1: normalised value k
+    TP(5);
     // layer 1: one-hot(dst) branch in lanes 0-31, buffers branch in lanes 32-63. The
     // buffers dot product runs with every lane active (lanes 0-31 discard it): its
     // readlanes read xn from lanes 1..deg, which must not sit in an inactive branch.
@@ -1540,9 +1566,11 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
             chunk(c, w);
         }
     }
+    TP(6);
     float h = det_elu(__fadd_rn(lane < 32 ? w1v : acc, b1v));
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
+    TP(7);
     TM_MLP(0);
     if constexpr (B != kMlpAll && PRISMA_MLP_PIPE) {
         // (half batches double-buffered: the same weight registers as B loads in flight)
@@ -1556,12 +1584,14 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
+    TP(8);
     TM_MLP(1);
     if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w3, M.b3));
     else h = det_elu(mlp_dense64<B>(S, RP + mlp_rp_layer_floats(64), lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
+    TP(9);
     TM_MLP(2);
     float q = 0.0f;
     if constexpr (B == kMlpAll) {
@@ -1571,10 +1601,12 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
         if (lane < deg) q = det_elu(mlp_dense64<B>(S, RP + 2 * mlp_rp_layer_floats(64), lane, D));
     }
     __builtin_amdgcn_wave_barrier();
+    TP(10);
     // tf.argmin: first minimum (learner.py:145)
     int best;
     if constexpr (B == kMlpAll) best = lane_argmin_first(q, deg);
     else best = lane_argmin_first_seq(q, deg);
+    TP(11);
     TM_MLP(3);
     return best;
 }
@@ -2207,6 +2239,8 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
     S.tsub[0] = 0; S.tsub[1] = 0; S.tlast = 0;
     S.tmlp[0] = 0; S.tmlp[1] = 0; S.tmlp[2] = 0; S.tmlp[3] = 0;
     S.tflow[0] = 0; S.tflow[1] = 0; S.tflow[2] = 0; S.tflow[3] = 0; S.tfl = 0;
+    for (int i = 0; i < 16; ++i) { S.tp[i] = 0; S.tpn[i] = 0; }
+    S.tpl = 0;
 #define TM_MARK(i) do { tm_b = TM_NOW(); tm_acc[i] += tm_b - tm_a; tm_cnt[i]++; tm_a = tm_b; } while (0)
 #else
 #define TM_MARK(i) do { } while (0)
@@ -2293,6 +2327,10 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
         }
         for (int i = 0; i < 4; ++i) atomicAdd(&g_prisma_timing[16 + i], (unsigned long long)S.tmlp[i]);
         for (int i = 0; i < 4; ++i) atomicAdd(&g_prisma_timing[20 + i], (unsigned long long)S.tflow[i]);
+        for (int i = 0; i < 16; ++i) {
+            atomicAdd(&g_prisma_timing[24 + i], (unsigned long long)S.tp[i]);
+            atomicAdd(&g_prisma_timing[40 + i], (unsigned long long)S.tpn[i]);
+        }
     }
 #endif
     if (!H.error) lazy_resolve(S, R, H, false);      // elided completions up to where the launch stopped

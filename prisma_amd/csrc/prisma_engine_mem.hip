@@ -546,8 +546,8 @@ extern "C" int prisma_debug_trace(void* dev_buf, unsigned int cap) {
 // diagnostic build only: read and clear the memory-resident engine's per-phase cycle totals
 extern "C" int prisma_debug_timing_mem(unsigned long long* out16) {
     if (hipDeviceSynchronize() != hipSuccess ||
-        hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prisma_timing), 32 * sizeof(unsigned long long)) != hipSuccess) return -1;
-    unsigned long long z[32] = {0};
+        hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_prisma_timing), kTimingWords * sizeof(unsigned long long)) != hipSuccess) return -1;
+    unsigned long long z[kTimingWords] = {0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

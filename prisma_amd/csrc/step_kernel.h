@@ -90,9 +90,9 @@ static const void* pick_step(int fs, int ls, bool tun) {
 #define PRISMA_TU_TIMING(NAME)                                                                          \
     extern "C" int NAME(unsigned long long* out32) {                                                    \
         if (hipDeviceSynchronize() != hipSuccess ||                                                     \
-            hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prisma_timing), 32 * sizeof(unsigned long long)) != \
+            hipMemcpyFromSymbol(out32, HIP_SYMBOL(g_prisma_timing), kTimingWords * sizeof(unsigned long long)) != \
                 hipSuccess) return -1;                                                                  \
-        unsigned long long z[32] = {0};                                                                 \
+        unsigned long long z[kTimingWords] = {0};                                                                 \
         return hipMemcpyToSymbol(HIP_SYMBOL(g_prisma_timing), z, sizeof(z)) == hipSuccess ? 0 : -1;     \
     }
 #else

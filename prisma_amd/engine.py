@@ -269,7 +269,8 @@ class PrismaEngine:
     def compact_pending(self, stream=None):
         """The pending replicas of the last step() as a dense batch (prisma_compact_pending):
         (ids int32 [n], obs int32 [n, W], node int32 [n]) for a policy that evaluates only the
-        notified replicas (ns3env.py:417-423). One host read of the count."""
+        notified replicas (ns3env.py:417-423). One host read of the count. The tensors are views
+        of buffers the next call reuses: valid until then (clone them to keep them longer)."""
         import torch
         if not hasattr(self, "_cids"):
             self._cids = torch.empty(self.R, dtype=torch.int32, device=self.torch_device)
@@ -280,6 +281,7 @@ class PrismaEngine:
                                            self._cids.data_ptr(), self._cobs.data_ptr(), self._cnode.data_ptr(),
                                            self._ccount.data_ptr(), _stream_handle(stream)))
         n = int(self._ccount.item())
+        self._cn = n
         return self._cids[:n], self._cobs[:n], self._cnode[:n]
 
     def expand_actions(self, ids, packed_actions, fill: int = 0, stream=None):
@@ -288,7 +290,16 @@ class PrismaEngine:
         import torch
         out = torch.empty(self.R, dtype=torch.int32, device=self.torch_device)
         n = int(ids.numel())
-        cnt = torch.tensor([n], dtype=torch.int32, device=self.torch_device)
+        # the count on the device without a host-to-device copy (a pageable copy synchronises the
+        # stream): compact_pending's own count when ids is its batch, else a device-side fill
+        if (hasattr(self, "_ccount") and n and n == self._cn and ids.data_ptr() == self._cids.data_ptr()
+                and ids.dtype == torch.int32):
+            cnt = self._ccount
+        else:
+            if not hasattr(self, "_ecount"):
+                self._ecount = torch.zeros(1, dtype=torch.int32, device=self.torch_device)
+            cnt = self._ecount
+            cnt.fill_(n)
         # (an empty batch still passes valid device pointers: the count says there is nothing)
         ids_c = ids.to(torch.int32).contiguous() if n else torch.zeros(1, dtype=torch.int32, device=self.torch_device)
         act = (packed_actions.to(torch.int32).contiguous() if n

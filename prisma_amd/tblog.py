@@ -473,6 +473,14 @@ def stats_writer_train(w_session: EventFileWriter, w_arrived: EventFileWriter, w
         wr.flush()
 
 
+def trainer_stats_writer(w: EventFileWriter, trainer, step: int) -> None:
+    """The trainer's own counters (QRoutingTrainer.stats(): signalling overheads, stored weight
+    generations, stale_syncs) under a "trainer/" prefix -- not tags of the reference's tb_logger."""
+    for k, v in trainer.stats().items():
+        w.scalar(f"trainer/{k}", float(v), step)
+    w.flush()
+
+
 def stats_writer_test(results_path: str, A: AgentStats, load_factor: float, model_version: str) -> str:
     """tb_logger.py:142-164: one writer under <results_path>/<model_version>, step = int(100 * load factor).
     Returns the events file path."""

@@ -93,6 +93,7 @@ latest gradient step (priority 1, as the loss transitions of forwarder.py:227-23
 from __future__ import annotations
 
 import copy
+import warnings
 from typing import Optional
 
 import numpy as np
@@ -261,7 +262,7 @@ class QRoutingTrainer:
                  big_signaling_size: int = 512, packet_size: int = 512, pending_cap: int = 1 << 20,
                  n_replicas: int = 1, signaling_sim: int = 1, sync_step: float = 1.0, sync_ratio: float = 0.1,
                  link_cap: int = 500000, link_delay_ms: float = 1.0, prioritized_replay: bool = False,
-                 max_snapshots: int = 32):
+                 max_snapshots: Optional[int] = None):
         if signaling_type not in ("ideal", "NN", "target"):
             raise ValueError("signaling_type must be 'ideal', 'NN' or 'target'")
         self.topo = topo
@@ -330,9 +331,13 @@ class QRoutingTrainer:
         # weights. The weights only change in place (train_step's Adam, a caller's edits), so syncs
         # between two changes share one stored generation (keyed on the parameters' in-place
         # version counters). Replica clocks drift apart, so the live versions grow towards O(R);
-        # max_snapshots caps the stored generations: at the cap a sync takes the newest stored
-        # generation instead of a new one (older weights by at most the syncs since it was taken).
-        self.max_snapshots = int(max_snapshots)
+        # max_snapshots (opt-in; None = unbounded, every sync copies the current weights as the
+        # reference's _sync_all does) caps the stored generations: at the cap a sync takes the
+        # newest stored generation instead of the current weights. Such syncs are counted in
+        # stale_syncs (stats(), tblog.trainer_stats_writer) and the first one warns.
+        self.max_snapshots = None if max_snapshots is None else int(max_snapshots)
+        self.stale_syncs = 0                         # syncs that received an older stored generation
+        self._stale_warned = False
         self._gen_w = {}                             # generation key -> stacked weights
         self._snap_gen = {}                          # version -> generation key
         self.version = 0
@@ -720,14 +725,29 @@ class QRoutingTrainer:
         return tuple(int(p._version) for p in self.params)
 
     def _capture(self):
-        """The generation key of the current online weights, stored if new (newest stored one at
-        the max_snapshots cap)."""
+        """The generation key of the current online weights, stored if new. At the opt-in
+        max_snapshots cap the newest stored generation instead (counted in stale_syncs)."""
         key = self._weights_key()
         if key not in self._gen_w:
-            if len(self._gen_w) >= self.max_snapshots:
+            if self.max_snapshots is not None and len(self._gen_w) >= self.max_snapshots:
+                self.stale_syncs += 1
+                if not self._stale_warned:
+                    warnings.warn(f"QRoutingTrainer: max_snapshots={self.max_snapshots} reached; syncs now copy "
+                                  "the newest stored weight generation instead of the current weights (counted "
+                                  "in stale_syncs). The reference copies the current weights at every sync "
+                                  "(trainer.py:101-171): leave max_snapshots=None for that", RuntimeWarning,
+                                  stacklevel=3)
+                    self._stale_warned = True
                 return self._snap_gen[max(self._snap_gen)]
             self._gen_w[key] = self._snapshot()
         return key
+
+    def stats(self) -> dict:
+        """The trainer's own counters (not the reference's Agent statistics): signalling overheads,
+        stored weight generations and the syncs that received an older generation (max_snapshots)."""
+        return {"small_signaling_bytes": float(self.small_overhead), "small_signaling_pkts": int(self.small_pkts),
+                "big_signaling_bits": float(self.big_overhead), "big_signaling_pkts": int(self.big_pkts),
+                "stored_generations": len(self._gen_w), "stale_syncs": int(self.stale_syncs)}
 
     def weights_of(self, version: int) -> dict:
         """The stacked online weights copy `version` refers to."""
@@ -735,7 +755,7 @@ class QRoutingTrainer:
 
     @property
     def snapshots(self) -> dict:
-        """Stored weight generations (bounded by max_snapshots)."""
+        """Stored weight generations (bounded by max_snapshots when it is set)."""
         return self._gen_w
 
     def _gc(self):
@@ -758,7 +778,6 @@ def train(env, trainer: QRoutingTrainer, steps: int, train_every: int = 1, sync_
     clock and ``QRoutingTrainer(sync_step=...)`` (trainer.py:101-112). Passing it warns and
     is otherwise ignored."""
     if sync_every is not None:
-        import warnings
         warnings.warn("train(sync_every=...) is ignored: syncs follow the replicas' simulated clocks; set "
                       "QRoutingTrainer(sync_step=seconds) instead", DeprecationWarning, stacklevel=2)
     obs, info = env.reset()

@@ -71,7 +71,7 @@ eng.reset(0)
 WARM = int(sys.argv[sys.argv.index("--warm") + 1]) if "--warm" in sys.argv else 1
 for _ in range(WARM):
     eng.run(table, HOPS)
-buf = (C.c_ulonglong * 48)()
+buf = (C.c_ulonglong * 64)()   # engine_core.h kTimingWords
 timing(buf)
 h0 = int(eng.counters()["hops_total"].sum())
 for _ in range(4):
@@ -92,8 +92,11 @@ if buf[20]:
     nf = buf[8 + 4]
     for i, nm in enumerate(["flow:record+block", "flow:send", "flow:draw", "flow:tree"]):
         print(f"  {nm:17s} cyc/flow={buf[20 + i] / max(1, nf):8.0f}")
-WAITS = ["arr:record", "arr:prev+obs", "send:record", "cmp:record", "cmp:ring", "flow:block+rec"]
-for i, nm in enumerate(WAITS):
-    if buf[32 + i]:
-        print(f"  wait {nm:15s} n/hop={buf[32 + i] / hops:.3f}  cyc/wait={buf[24 + i] / buf[32 + i]:8.0f}  "
-              f"share={buf[24 + i] / tot:.3f}")
+# fine probes TP(i) (engine_core.h): cycles since the previous probe, per execution
+PROBES = ["mlp:wait-arrival", "mlp:sum", "mlp:w3-issue", "mlp:var", "mlp:w4-issue", "mlp:den+xn",
+          "mlp:l1-chunks", "mlp:l1-elu+store", "mlp:l2", "mlp:l3", "mlp:l4", "mlp:argmin",
+          "dec:send", "dec:record+cnt", "probe14", "probe15"]
+for i, nm in enumerate(PROBES):
+    n = buf[40 + i]
+    if n:
+        print(f"  probe {nm:17s} n/hop={n / hops:.3f}  cyc/call={buf[24 + i] / n:8.0f}  share={buf[24 + i] / tot:.3f}")

@@ -107,3 +107,23 @@ def test_bench_launcher_deadline_names_stalled_rank():
     assert p.returncode == 124, (p.returncode, p.stderr[-2000:])
     assert wall < deadline + 20.0
     assert "rank 1 (last stage: started)" in p.stderr and "rank 0 (last stage: started)" in p.stderr
+
+
+@pytest.mark.parametrize("preset", ["config4", "config5"])
+def test_bench_presets_rendezvous_gloo_world2(preset):
+    """The 8-GPU presets resolve to BASELINE config 4 / 5 per GPU (weak scaling) on every rank:
+    two gloo ranks rendezvous, all-gather their replica shards, and rank 0 reports the workload."""
+    import json
+    p, _ = _bench(["--gpus", "2", "--rendezvous-only", "--backend", "gloo", "--preset", preset,
+                   "--rank-deadline", "120"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    w = d["workload"]
+    assert d["world_size"] == 2 and w["preset"] == preset and w["policy"] == "dqn_buffer"
+    if preset == "config4":
+        assert w["topology"] == "geant" and w["ping_as_obs"] == 0 and w["replicas_per_gpu"] == 2048
+        assert w["load_factors"] == [0.5, 0.75, 1.0, 1.25, 1.5, 1.75, 2.0]
+        assert d["replicas_gathered"] == 4096
+    else:
+        assert w["topology"] == "er256" and w["ping_as_obs"] == 1 and w["replicas_per_gpu"] == 1024
+        assert w["load_factors"] == [1.0] and d["replicas_gathered"] == 2048 and w["warmup"] == 13

@@ -177,3 +177,24 @@ def test_bench_rccl_one_rank_group(mode):
     else:
         assert d["dist"] == {"world_size": 1, "backend": "nccl", "replicas_gathered": 128}
         assert d["errors"] == 0 and d["replicas_total"] == 128
+
+
+@pytest.mark.parametrize("preset,lfs", [("config4", "0.5,2.0"), ("config5", None)])
+def test_bench_presets_two_ranks_same_device(preset, lfs):
+    """The 8-GPU presets as one command each (bench.py --preset config4 / config5), rehearsed with
+    two ranks on cuda:0 at a small replica count: config 4 prints one line per load factor of its
+    sweep, config 5 runs the ER-256 DQN-buffer workload on the memory-resident engine."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--same-device", "--preset", preset,
+           "--steps", "2", "--warmup", "1", "--replicas", "16", "--hops", "256", "--cpu-baseline", "0"]
+    if lfs:
+        cmd += ["--load-factors", lfs]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [json.loads(ln) for ln in p.stdout.splitlines() if ln.startswith("{")]
+    want = [float(x) for x in lfs.split(",")] if lfs else [1.0]
+    assert [d["config"]["load_factor"] for d in lines] == want
+    for d in lines:
+        assert d["config"]["preset"] == preset and d["replicas_total"] == 32 and d["errors"] == 0
+        assert d["config"]["policy"] == "dqn_buffer" and d["config"]["replicas_per_gpu"] == 16
+        assert d["config"]["topology"] == ("geant" if preset == "config4" else "er256")
+        assert "mem_step" in d["roofline"]["kernel"] if preset == "config5" else "step_kernel_t<8" in d["roofline"]["kernel"]

@@ -560,15 +560,17 @@ def test_snapshot_generations_stay_bounded_with_drifting_clocks():
     clock = np.zeros(R)
     speed = rng.random(R) * 0.004
     g = torch.Generator().manual_seed(1)
-    for step in range(60):
-        clock += speed
-        tr.advance_clock(torch.from_numpy((clock * 1e9).astype(np.int64)))
-        tr.check_sync()
-        if step % 3 == 0:                                           # an optimizer step now and then
-            with torch.no_grad():
-                for p in tr.q.parameters():
-                    p.add_(1e-3 * torch.randn(p.shape, generator=g))
-        assert len(tr.snapshots) <= 8, (step, len(tr.snapshots))
+    with pytest.warns(RuntimeWarning, match="max_snapshots=8 reached"):
+        for step in range(60):
+            clock += speed
+            tr.advance_clock(torch.from_numpy((clock * 1e9).astype(np.int64)))
+            tr.check_sync()
+            if step % 3 == 0:                                       # an optimizer step now and then
+                with torch.no_grad():
+                    for p in tr.q.parameters():
+                        p.add_(1e-3 * torch.randn(p.shape, generator=g))
+            assert len(tr.snapshots) <= 8, (step, len(tr.snapshots))
+    assert tr.stale_syncs > 0 and tr.stats()["stale_syncs"] == tr.stale_syncs   # the cap was forced
     assert len(set(tr.tgt_ver.ravel().tolist()) | set(tr.up_ver.ravel().tolist())) > 8   # many versions...
     # ...each resolving to stored weights, and targets() runs one pass per stored generation
     B = 64
@@ -585,6 +587,47 @@ def test_snapshot_generations_stay_bounded_with_drifting_clocks():
         want = tr._bootstrap(net, node[j:j + 1], action[j:j + 1], torch.zeros(1), nobs[j:j + 1],
                              torch.zeros(1, dtype=torch.bool))
         assert torch.allclose(got[j:j + 1], want, rtol=1e-6, atol=1e-6), (got[j], want)
+
+
+def test_syncs_copy_the_current_weights_without_a_cap():
+    """Default (max_snapshots=None): every sync's copy is the online weights at that sync, as the
+    reference's _sync_all copies them (trainer.py:101-171), and no sync is counted stale."""
+    import warnings as _w
+    topo = Topology.example("abilene")
+    R = 64
+    tr = QRoutingTrainer(topo, "buffer", seed=4, device="cpu", n_replicas=R, sync_step=0.01, batch_size=4)
+    rng = np.random.default_rng(7)
+    clock = np.zeros(R)
+    speed = rng.random(R) * 0.004
+    g = torch.Generator().manual_seed(2)
+    syncs = 0
+    with _w.catch_warnings():
+        _w.simplefilter("error", RuntimeWarning)
+        for step in range(60):
+            clock += speed
+            tr.advance_clock(torch.from_numpy((clock * 1e9).astype(np.int64)))
+            v0 = tr.version
+            tr.check_sync()
+            cur = {k: t.detach().clone() for k, t in tr.q.state_dict().items()}
+            if tr.version != v0:
+                syncs += 1
+                for k, t in tr.weights_of(tr.version).items():       # this sync's copy == the weights now
+                    assert torch.equal(t, cur[k]), (step, k)
+            with torch.no_grad():                                     # an optimizer step after every sync
+                for p in tr.q.parameters():
+                    p.add_(1e-3 * torch.randn(p.shape, generator=g))
+    assert syncs > 32 and tr.stale_syncs == 0 and tr.stats()["stale_syncs"] == 0
+
+
+def test_trainer_stats_tblog(tmp_path):
+    from prisma_amd import tblog
+    topo = Topology.example("abilene")
+    tr = QRoutingTrainer(topo, "buffer", seed=0, device="cpu")
+    w = tblog.EventFileWriter(str(tmp_path))
+    tblog.trainer_stats_writer(w, tr, 3)
+    w.close()
+    tags = {t for e in tblog.read_events(w.path) for (t, _, _) in e["values"]}
+    assert tags == {f"trainer/{k}" for k in tr.stats()}
 
 
 def test_trainer_replica_count_must_match_the_env():
