@@ -65,6 +65,20 @@ static __device__ unsigned long long g_prisma_timing[kTimingWords];
 #define TP_START() do { } while (0)
 #define TP(i) do { } while (0)
 #endif
+// probe sets (timing build, -DPRISMA_TP_SET): 0 the decision (mlp_action, apply_decision), 1 the
+// memory-resident arrival / completion / flow handlers
+#ifndef PRISMA_TP_SET
+#define PRISMA_TP_SET 0
+#endif
+#if PRISMA_TP_SET == 0
+#define TP0(i) TP(i)
+#define TP1(i) do { } while (0)
+#define TP1_START() do { } while (0)
+#else
+#define TP0(i) do { } while (0)
+#define TP1(i) TP(i)
+#define TP1_START() TP_START()
+#endif
 
 // ---------------------------------------------------------------------------
 // kernel parameters
@@ -491,6 +505,10 @@ __device__ __forceinline__ uint32_t ring_cap(const Sim& S, uint32_t l) {
 }
 
 // one link's fields as uniform scalars
+// an observation gather in flight (memory-resident engine, PRISMA_OBS_EARLY): the link-record
+// words of lane i's out-link (queued bytes, or the ping words)
+struct ObsG { uint32_t a, b, c, d, e; };
+
 struct LinkV {
     uint32_t head, txp, tail, n_wire, n_queue, busy, qb;
     uint32_t cp_t, cp_seq;       // completion time (low 32 bits), seq
@@ -786,19 +804,24 @@ __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l
 template <class RS>
 __device__ __forceinline__ void on_complete(const Sim& S, RS& R, Hot& H, uint32_t l) {   // :305-336
     const LV& L = S.lv;
+    if (S.mem) TP1_START();
     LinkV k = link_get(R, l);
     k.busy = 0;
+    if (S.mem) TP1(7);
     if (k.n_queue) {
         uint32_t cap = ring_cap(S, l);
         uint32_t xi = k.txp;
         uint32_t hx = u_ld32(&S.ring[ring_off(S, l) + xi]);
+        if (S.mem) TP1(8);
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
         k.qb -= ent_size(S, hx, l);
         transmit_start(S, H, l, k, xi, hx);
     }
+    if (S.mem) TP1(9);
     link_put(S, R, H, l, k);
+    if (S.mem) TP1(10);
 }
 
 // ---- observation (data-packet-manager.cc:171-206)
@@ -864,6 +887,22 @@ __device__ __forceinline__ uint32_t observe_links(const Sim& S, const Regs<FS, L
     return (lane >= 1 && lane <= deg) ? o : 0u;
 }
 
+#ifndef PRISMA_NT_LOG
+#define PRISMA_NT_LOG 0
+#endif
+#ifndef PRISMA_NT_PREV
+#define PRISMA_NT_PREV 0
+#endif
+typedef unsigned int nt_u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int nt_u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 ld_nt4(const void* p) {
+    const nt_u32x4 v = __builtin_nontemporal_load((const nt_u32x4*)p);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 ld_nt2(const void* p) {
+    const nt_u32x2 v = __builtin_nontemporal_load((const nt_u32x2*)p);
+    return make_uint2(v.x, v.y);
+}
 // one coalesced wave store of a decision record (lane i writes word i)
 __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_t d, double reward, uint32_t uid,
                                              int32_t prev, uint32_t node, uint32_t dst, uint32_t start, int action,
@@ -887,7 +926,12 @@ __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_
     uint32_t ob = bperm(obs_reg, (uint32_t)(lane - 8) & 63u);
     uint32_t word = bfi(S.m8, hw, ob);
     uint32_t* p = (uint32_t*)(S.logrep + (size_t)(d & (S.lv.log_cap() - 1)) * S.lv.rec_bytes());
-    if (lane < 8 + S.lv.W()) p[lane] = word;
+    if (lane < 8 + S.lv.W()) {
+        // PRISMA_NT_LOG: the log is streamed out (read back once, long after): a non-temporal
+        // store keeps it from displacing the replica state in the caches
+        if (PRISMA_NT_LOG) __builtin_nontemporal_store(word, p + lane);
+        else p[lane] = word;
+    }
 }
 
 // action + status of a record written earlier (TTL and episode bytes kept)
@@ -995,14 +1039,14 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
 #if PRISMA_TIMING
     { const uint64_t t = TM_NOW(); S.tsub[0] += t - S.tlast; S.tlast = t; }
 #endif
-    TP(12);
+    TP0(12);
     if (fused) write_record(S, H, d, reward, uid, prev, v, dst, start, action, status, obs_reg, ttl);
     else patch_record(S, H, d, action, status);
     receive_counters(S, R, H, x, false, 0u, 0u);
 #if PRISMA_TIMING
     { const uint64_t t = TM_NOW(); S.tsub[1] += t - S.tlast; S.tlast = t; }
 #endif
-    TP(13);
+    TP0(13);
 }
 
 // Answer to the pending notification.  Returns 1 if a hop was executed (0 for a
@@ -1283,6 +1327,29 @@ __device__ __forceinline__ void mlp_preload_w4(MlpPre& M, const float* __restric
 // known, has_w1): issued by the memory-resident engine's arrival handler together with
 // its second round trip (previous decision record, observation), so the decision finds
 // them in registers
+// PRISMA_PRE_W2: layer 2's weights ride along the arrival's second round trip (1) or are issued when
+// the decision starts (0, round 5: +4.8 % at config 5 -- the arrival's gather no longer waits behind
+// 17 weight loads, and their 64 VGPRs are not held across the arrival's tree repair)
+#ifndef PRISMA_PRE_W2
+#define PRISMA_PRE_W2 0
+#endif
+#ifndef PRISMA_OBS_EARLY
+#define PRISMA_OBS_EARLY 0
+#endif
+#ifndef PRISMA_PRE_AFTER_OBS
+#define PRISMA_PRE_AFTER_OBS 0
+#endif
+#ifndef PRISMA_MLP_CHAINS
+#define PRISMA_MLP_CHAINS 1
+#endif
+// where the memory-resident engine issues layer 3's / layer 4's weights: 0 inside the LayerNorm
+// (after its first / second sum), 1 when layer 1 ends, 2 (layer 4 only) when layer 2 ends
+#ifndef PRISMA_W3_AT
+#define PRISMA_W3_AT 0
+#endif
+#ifndef PRISMA_W4_AT
+#define PRISMA_W4_AT 0
+#endif
 __device__ __forceinline__ void mlp_preload_node(MlpPre1& M, const Sim& S, uint32_t v, uint32_t dst, bool has_w1) {
     const int lane = S.lane;
     v = rfl(v);                  // uniform: the row pointers come from scalar loads
@@ -1293,9 +1360,11 @@ __device__ __forceinline__ void mlp_preload_node(MlpPre1& M, const Sim& S, uint3
     M.has_w1 = has_w1;
     M.w1v = 0.0f;
     if (has_w1 && lane < 32) M.w1v = S.mlp[((int)v * S.lv.N() + (int)dst) * 32 + (lane & 31)];
+    if (PRISMA_PRE_W2) {
 #pragma unroll
-    for (int c = 0; c < 16; ++c) M.w2[c] = ((const float4*)RP)[c * 64 + lane];
-    M.b2 = RP[64 * 64 + lane];
+        for (int c = 0; c < 16; ++c) M.w2[c] = ((const float4*)RP)[c * 64 + lane];
+        M.b2 = RP[64 * 64 + lane];
+    }
     const int j32 = lane & 31, nck = (deg + 3) >> 2;
     const float4* __restrict__ Wb4 = (const float4*)RP1;
 #pragma unroll
@@ -1305,6 +1374,22 @@ __device__ __forceinline__ void mlp_preload_node(MlpPre1& M, const Sim& S, uint3
 
 __device__ __forceinline__ float mlp_dense64_pre(const Sim& S, const float4 (&w)[16], float b) {
     const float4* __restrict__ hb = (const float4*)S.hbuf;
+    if (PRISMA_MLP_CHAINS == 2) {            // (perf experiment: two chains, even / odd chunks)
+        float a0 = 0.0f, a1 = 0.0f;
+#pragma unroll
+        for (int c = 0; c < 16; c += 2) {
+            const float4 h0 = hb[c], h1 = hb[c + 1];
+            a0 = __builtin_fmaf(h0.x, w[c].x, a0);
+            a1 = __builtin_fmaf(h1.x, w[c + 1].x, a1);
+            a0 = __builtin_fmaf(h0.y, w[c].y, a0);
+            a1 = __builtin_fmaf(h1.y, w[c + 1].y, a1);
+            a0 = __builtin_fmaf(h0.z, w[c].z, a0);
+            a1 = __builtin_fmaf(h1.z, w[c + 1].z, a1);
+            a0 = __builtin_fmaf(h0.w, w[c].w, a0);
+            a1 = __builtin_fmaf(h1.w, w[c + 1].w, a1);
+        }
+        return __fadd_rn(__fadd_rn(a0, a1), b);
+    }
     float acc = 0.0f;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -1435,6 +1520,44 @@ __device__ __forceinline__ int lane_argmin_first(float q, int n) {
     return (int)__builtin_ctzll(__ballot(key == kmin));
 }
 
+// LayerNorm and layer 1 from LDS (the memory-resident engine, PRISMA_LN_LDS): the deg buffer
+// values (and later their squared deviations and normalised values) sit at hbuf[0..deg-1], +0
+// past the degree, and every lane reads them back as 16-B broadcasts -- the sums and the layer-1
+// FMA chain run in the oracle's order on VGPR operands instead of a v_readlane per term.  A +0 term
+// is an exact identity here: the sums start at +0 and add non-negative values (never -0), and
+// fma(+0, w, acc) = acc for finite w and acc != -0 (acc starts at +0 and an exact cancellation
+// rounds to +0).
+#ifndef PRISMA_LN_LDS
+#define PRISMA_LN_LDS 1
+#endif
+#ifndef PRISMA_LN_LDS_REG
+#define PRISMA_LN_LDS_REG 0
+#endif
+__device__ __forceinline__ float lds_sum_ordered(const float4* hb4, int nck) {
+    float4 h[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) h[c] = hb4[c];                      // 32 slots, all written
+    float s = 0.0f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+        if (c >= nck) break;                                        // uniform
+        s = __fadd_rn(s, h[c].x); s = __fadd_rn(s, h[c].y); s = __fadd_rn(s, h[c].z); s = __fadd_rn(s, h[c].w);
+    }
+    for (int c = 8; c < nck; ++c) {                                 // degrees beyond 32
+        const float4 g = hb4[c];
+        s = __fadd_rn(s, g.x); s = __fadd_rn(s, g.y); s = __fadd_rn(s, g.z); s = __fadd_rn(s, g.w);
+    }
+    return s;
+}
+// a / d for an integer d (the node's degree) with rd = RN(1/d): q = a rd and one FMA correction
+// (Markstein), the correctly rounded quotient for 2^-120 <= a (and a = 0) and 1 <= d <= 64 --
+// checked exhaustively over every float a in that range (tests/test_numerics_division.py)
+__device__ __forceinline__ float div_deg(float a, float d, float rd) {
+    const float q = __fmul_rn(a, rd);
+    const float e = __builtin_fmaf(-q, d, a);
+    return __builtin_fmaf(e, rd, q);
+}
+
 template <int B, bool PRE = false>
 __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs_reg, const MlpPre1& P1) {
     const LV& L = S.lv;
@@ -1454,11 +1577,11 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
 #else
 #define TM_MLP(i) do { } while (0)
 #endif
-    TP_START();
+    if (PRISMA_TP_SET == 0) TP_START();
 #if PRISMA_TIMING
     if constexpr (PRE) __builtin_amdgcn_s_waitcnt(0);     // the arrival's loads (probe only)
 #endif
-    TP(0);
+    TP0(0);
     const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
     const uint32_t dst = rdl(obs_reg, 0);
     // layer-1 weights first (independent of the normalisation): one W1 row element and
@@ -1489,6 +1612,12 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     // two halves inside the LayerNorm below, so their issue overlaps its dependent chain instead
     // of holding the wave in front of it
     if constexpr (B == kMlpAll && !PRE) mlp_preload(M, RP, lane, D, deg, true);
+    if constexpr (B == kMlpAll && PRE && !PRISMA_PRE_W2) {
+#pragma unroll
+        for (int c = 0; c < 16; ++c) M.w2[c] = ((const float4*)RP)[c * 64 + lane];
+        M.b2 = RP[64 * 64 + lane];
+        __builtin_amdgcn_sched_barrier(0);
+    }
     float b1v;
     float4 wb[4];
     if constexpr (PRE) {
@@ -1511,33 +1640,54 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     // (the memory-resident engine's single wave per SIMD gains from the 4-wide sums and the
     // DPP argmin below; the register-resident MLP instances lost 1 % with them, A/B on GEANT)
     const float xf = (float)obs_reg;
+    // (PRISMA_LN_LDS_REG: the register-resident instances too)
+    constexpr bool kLnLds = (B == kMlpAll || PRISMA_LN_LDS_REG) && PRISMA_LN_LDS;
+    const float4* hb4 = (const float4*)S.hbuf;
+    const bool inb = lane >= 1 && lane <= deg;
+    const float fdeg = (float)deg;
+    float rdeg = 0.0f;
     float sum = 0.0f;
-    if constexpr (B == kMlpAll) sum = lane_sum_ordered(xf, deg);
+    if constexpr (kLnLds) {
+        rdeg = __fdiv_rn(1.0f, fdeg);                               // off the sums' chain
+        S.hbuf[(lane - 1) & 63] = inb ? xf : 0.0f;                  // value k at hbuf[k]
+        __builtin_amdgcn_wave_barrier();
+        sum = lds_sum_ordered(hb4, nck);
+    } else if constexpr (B == kMlpAll) sum = lane_sum_ordered(xf, deg);
     else for (int k = 0; k < deg; ++k) sum = __fadd_rn(sum, rdlf(xf, (uint32_t)(k + 1)));
-    TP(1);
-    if constexpr (B == kMlpAll && PRE) {
+    TP0(1);
+    if constexpr (B == kMlpAll && PRE && PRISMA_W3_AT == 0) {
         __builtin_amdgcn_sched_barrier(0);
         mlp_preload_w3(M, RP, lane);
         __builtin_amdgcn_sched_barrier(0);
     }
-    TP(2);
-    const float mean = __fdiv_rn(sum, (float)deg);
+    TP0(2);
+    const float mean = kLnLds ? div_deg(sum, fdeg, rdeg) : __fdiv_rn(sum, (float)deg);
     const float dv = __fsub_rn(xf, mean);
     const float sq = __fmul_rn(dv, dv);
     float var = 0.0f;
-    if constexpr (B == kMlpAll) var = lane_sum_ordered(sq, deg);
+    if constexpr (kLnLds) {
+        __builtin_amdgcn_wave_barrier();
+        S.hbuf[(lane - 1) & 63] = inb ? sq : 0.0f;
+        __builtin_amdgcn_wave_barrier();
+        var = lds_sum_ordered(hb4, nck);
+    } else if constexpr (B == kMlpAll) var = lane_sum_ordered(sq, deg);
     else for (int k = 0; k < deg; ++k) var = __fadd_rn(var, rdlf(sq, (uint32_t)(k + 1)));
-    TP(3);
-    if constexpr (B == kMlpAll && PRE) {
+    TP0(3);
+    if constexpr (B == kMlpAll && PRE && PRISMA_W4_AT == 0) {
         __builtin_amdgcn_sched_barrier(0);
         mlp_preload_w4(M, RP, lane, D, deg);
         __builtin_amdgcn_sched_barrier(0);
     }
-    TP(4);
-    var = __fdiv_rn(var, (float)deg);
+    TP0(4);
+    var = kLnLds ? div_deg(var, fdeg, rdeg) : __fdiv_rn(var, (float)deg);
     const float den = __fsqrt_rn(__fadd_rn(var, 1e-3f));
     const float xn = __fdiv_rn(dv, den);                          // lane k+1: normalised value k
-    TP(5);
+    if constexpr (kLnLds) {
+        __builtin_amdgcn_wave_barrier();
+        S.hbuf[(lane - 1) & 63] = inb ? xn : 0.0f;
+        __builtin_amdgcn_wave_barrier();
+    }
+    TP0(5);
     // layer 1: one-hot(dst) branch in lanes 0-31, buffers branch in lanes 32-63. The
     // buffers dot product runs with every lane active (lanes 0-31 discard it): its
     // readlanes read xn from lanes 1..deg, which must not sit in an inactive branch.
@@ -1549,7 +1699,25 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
         if (k + 2 < deg) acc = __builtin_fmaf(rdlf(xn, (uint32_t)(k + 3)), w.z, acc);
         if (k + 3 < deg) acc = __builtin_fmaf(rdlf(xn, (uint32_t)(k + 4)), w.w, acc);
     };
-    if constexpr (B == kMlpAll) {
+    if constexpr (kLnLds) {
+        // every term of a chunk (+0 past the degree), the inputs as LDS broadcasts
+        auto chunk4 = [&](const float4& x, const float4& w) {
+            acc = __builtin_fmaf(x.x, w.x, acc);
+            acc = __builtin_fmaf(x.y, w.y, acc);
+            acc = __builtin_fmaf(x.z, w.z, acc);
+            acc = __builtin_fmaf(x.w, w.w, acc);
+        };
+        float4 h[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) h[c] = hb4[c];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            if (c >= nck) break;
+            if constexpr (B == kMlpAll) chunk4(h[c], c < 4 ? wb[c & 3] : wx[c & 3]);
+            else chunk4(h[c], c < 4 ? wb[c & 3] : Wb4[c * 32 + j32]);
+        }
+        for (int c = 8; c < nck; ++c) chunk4(hb4[c], Wb4[c * 32 + j32]);
+    } else if constexpr (B == kMlpAll) {
         // chunks named at compile time (a runtime-indexed select over wb/wx put them on the stack)
 #pragma unroll
         for (int c = 0; c < 8; ++c)
@@ -1566,32 +1734,49 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
             chunk(c, w);
         }
     }
-    TP(6);
+    TP0(6);
     float h = det_elu(__fadd_rn(lane < 32 ? w1v : acc, b1v));
+    if constexpr (kLnLds) __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
-    TP(7);
+    TP0(7);
     TM_MLP(0);
+    if constexpr (B == kMlpAll && PRE && PRISMA_W3_AT == 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        mlp_preload_w3(M, RP, lane);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (B == kMlpAll && PRE && PRISMA_W4_AT == 1) {
+        __builtin_amdgcn_sched_barrier(0);
+        mlp_preload_w4(M, RP, lane, D, deg);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     if constexpr (B != kMlpAll && PRISMA_MLP_PIPE) {
         // (half batches double-buffered: the same weight registers as B loads in flight)
         const float q4 = mlp_l234_pipe<kPipeB, kPipeEarly>(S, RP, lane, D, deg, w20);
         __builtin_amdgcn_wave_barrier();
         return lane_argmin_first_seq(q4, deg);
     }
-    if constexpr (PRE) h = det_elu(mlp_dense64_pre(S, P1.w2, P1.b2));
+    if constexpr (PRE && PRISMA_PRE_W2) h = det_elu(mlp_dense64_pre(S, P1.w2, P1.b2));
+    else if constexpr (PRE) h = det_elu(mlp_dense64_pre(S, M.w2, M.b2));
     else if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w2, M.b2));
     else h = det_elu(mlp_dense64<B>(S, RP, lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
-    TP(8);
+    TP0(8);
     TM_MLP(1);
+    if constexpr (B == kMlpAll && PRE && PRISMA_W4_AT == 2) {
+        __builtin_amdgcn_sched_barrier(0);
+        mlp_preload_w4(M, RP, lane, D, deg);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w3, M.b3));
     else h = det_elu(mlp_dense64<B>(S, RP + mlp_rp_layer_floats(64), lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
-    TP(9);
+    TP0(9);
     TM_MLP(2);
     float q = 0.0f;
     if constexpr (B == kMlpAll) {
@@ -1601,12 +1786,12 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
         if (lane < deg) q = det_elu(mlp_dense64<B>(S, RP + 2 * mlp_rp_layer_floats(64), lane, D));
     }
     __builtin_amdgcn_wave_barrier();
-    TP(10);
+    TP0(10);
     // tf.argmin: first minimum (learner.py:145)
     int best;
     if constexpr (B == kMlpAll) best = lane_argmin_first(q, deg);
     else best = lane_argmin_first_seq(q, deg);
-    TP(11);
+    TP0(11);
     TM_MLP(3);
     return best;
 }
@@ -1704,12 +1889,26 @@ template <bool PRE = false, class RS>
 __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l, Decision& D, bool fused,
                                          MlpPre1& Mpre) {
     const LV& L = S.lv;
+    if (S.mem) TP1_START();
     const uint32_t v = (uint32_t)t_ldst(S, l);
-    LinkV k = link_get(R, l);
+    // memory-resident engine (PRISMA_OBS_EARLY): node v's observation is gathered before the
+    // arrival link's record comes back -- it depends on v alone, and nothing this arrival does
+    // before a decision writes v's out-links -- so its round trip overlaps the record's; the
+    // arrivals that decide nothing (pings, packets at their destination) discard it
+    ObsG og;
+    LinkV k;
+    if constexpr (RS::kMem && PRISMA_OBS_EARLY) {
+        const uint32_t rec = rec_load(R, l);                        // issued first ...
+        og = obs_issue(S, R, v);                                    // ... the gather behind it
+        k = link_fields(R, rec);                                    // waits for the record only
+    } else {
+        k = link_get(R, l);
+    }
     const uint32_t wh = k.head & (uint32_t)(L.WCAP() - 1);
     const uint32_t x = S.mem ? wire_ent(S, k, wh)
                              : (S.tun ? u_ld32(&S.went[l * (uint32_t)L.WCAP() + wh])
                                       : u_ld32(&S.ring[ring_off(S, l) + k.head]));
+    if (S.mem) TP1(0);
     const uint32_t type = ent_type(x);
     const bool tun = S.tun;
     if (ent_is_data(x)) {
@@ -1725,9 +1924,9 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         const uint32_t d = H.dec;
         const uint32_t dist = (d - r_dec(x)) & kRelayMask;
         const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap() - 1)) * L.rec_bytes();
-        const uint4 ph = *(const uint4*)pr;
-        const uint2 pw = *(const uint2*)(pr + 24);
-        if constexpr (PRE) {                                        // the decision's weights ride along
+        const uint4 ph = PRISMA_NT_PREV ? ld_nt4(pr) : *(const uint4*)pr;
+        const uint2 pw = PRISMA_NT_PREV ? ld_nt2(pr + 24) : *(const uint2*)(pr + 24);
+        if (PRE && !PRISMA_PRE_AFTER_OBS) {                         // the decision's weights ride along
             if (S.ctrl) {
                 mlp_preload_node(Mpre, S, v, 0u, false);
             } else {
@@ -1740,8 +1939,20 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         // memory-resident engine: the observation's gather goes out with the record
         // load, before the arrival link's update (it reads node v's out-links, which
         // nothing touches before the decision)
-        const uint32_t obs_early = S.mem ? observe_links(S, R, H, v, ns_to_sec(H.now)) : 0u;
+        uint32_t obs_early = 0u;
+        if constexpr (RS::kMem && PRISMA_OBS_EARLY) obs_early = obs_finish(S, R, H, v, og, ns_to_sec(H.now));
+        else if (S.mem) obs_early = observe_links(S, R, H, v, ns_to_sec(H.now));
+        if (PRE && PRISMA_PRE_AFTER_OBS) {          // (issued behind the gather: the arrival does not wait for them)
+            if (S.ctrl) {
+                mlp_preload_node(Mpre, S, v, 0u, false);
+            } else {
+                const uint32_t dst_e = (type == T_FRESH) ? f_dst(x) : r_dst(x);
+                if (dst_e != v) mlp_preload_node(Mpre, S, v, dst_e, true);
+            }
+        }
+        if (S.mem) TP1(1);
         wire_pop(S, R, H, l, k);
+        if (S.mem) TP1(2);
         uint32_t ttl = 255u;                                        // SetIpTtl(255) (poisson-application.cc:330)
         if (tun && type == T_RELAY) {
             // Tunnelled overlay: the packet's next hop is the target of the tunnel
@@ -1779,6 +1990,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         const uint32_t obs_links = S.mem ? obs_early : observe_links(S, R, H, v, ns_to_sec(H.now));
         const int64_t t_prev = mk64(rfl(ph.x), rfl(ph.y));
         const uint32_t uid_prev = rfl(ph.z), w_prev = rfl(pw.x);
+        if (S.mem) TP1(3);
         double reward = 0.0;
         int32_t prev = -1;
         uint32_t dst, start, uid, last = 0u;
@@ -1822,9 +2034,11 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
             return 0;
         }
         if (!fused) write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_PENDING, o, ttl);
+        if (S.mem) TP1(4);
         return 1;
     }
     wire_pop(S, R, H, l, k);
+    if (S.mem) TP1(5);
     if (S.ctrl && ent_is_big(x)) {                                  // (only with --signaling and --train)
         const uint32_t bp = t_bpair(S, g_gen(x));
         const uint32_t src = bp_src(bp), dst = bp_dst(bp);
@@ -1895,6 +2109,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         if (org != v) { ctrl_forward(S, R, H, v, org, x); return 0; }
     }
     receive_counters(S, R, H, x, false, 0u, l);
+    if (S.mem) TP1(6);
     return 0;
 }
 

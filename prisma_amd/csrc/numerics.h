@@ -106,7 +106,33 @@ __host__ __device__ inline float det_expm1f(float x) {
 }
 
 // Keras ELU (alpha 1): x > 0 ? x : expm1(x)
-__host__ __device__ inline float det_elu(float x) { return x > 0.0f ? x : det_expm1f(x); }
+#ifndef PRISMA_ELU_SELECT
+#define PRISMA_ELU_SELECT 0
+#endif
+__host__ __device__ inline float det_elu(float x) {
+#if defined(__HIP_DEVICE_COMPILE__) && PRISMA_ELU_SELECT
+    // det_expm1f's operations on every lane and its cases as selects (no exec-mask branches);
+    // the selected value is the same operation sequence's, so the bits equal det_elu's
+    const float t = x * 1.44269504f + 0.5f;
+    int ki = (int)t;
+    ki = ((float)ki > t) ? ki - 1 : ki;
+    const float k = (float)ki;
+    const float r = (x - k * 0.693145751953125f) - k * 1.42860677e-06f;
+    float p = r * 1.98412698e-04f;
+    p = (p + 1.38888889e-03f) * r;
+    p = (p + 8.33333333e-03f) * r;
+    p = (p + 4.16666667e-02f) * r;
+    p = (p + 1.66666667e-01f) * r;
+    p = (p + 0.5f) * r;
+    p = (p + 1.0f) * r;
+    const float scale = __builtin_bit_cast(float, (uint32_t)(127 + ki) << 23);
+    const float e = (ki == 0) ? p : scale * (p + 1.0f) - 1.0f;
+    const float m = (x < -17.0f) ? -1.0f : ((x > -5.9604645e-08f) ? x : e);
+    return (x > 0.0f || !(x == x)) ? x : m;
+#else
+    return x > 0.0f ? x : det_expm1f(x);
+#endif
+}
 
 // ns-3 Seconds(double) -> int64 ns (round to nearest)
 __host__ __device__ inline int64_t sec_to_ns(double s) { return (int64_t)(s * 1e9 + 0.5); }

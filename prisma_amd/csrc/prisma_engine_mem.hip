@@ -37,7 +37,17 @@ struct MemSt {
     // of storing the new key and loading the block back (one HBM round trip per flow event)
     uint4 fblk;
     uint32_t fblk_b;             // its block index, or ~0u
+    // PRISMA_TOP_REG: the tree's top level (level 2, n2 <= 64 group minima) in VGPRs, lane g =
+    // group g {t lo, t hi, seq, code}, loaded from the LDS image when a launch starts and written
+    // back when it ends: selecting an event and repairing level 2 need no LDS round trip
+    uint32_t g_tlo, g_thi, g_s, g_c;
 };
+#ifndef PRISMA_TOP_REG
+#define PRISMA_TOP_REG 0
+#endif
+#ifndef PRISMA_BLK_UNIFORM
+#define PRISMA_BLK_UNIFORM 0
+#endif
 
 constexpr int64_t kInf = INT64_MAX;
 
@@ -105,6 +115,15 @@ __device__ __forceinline__ Key block_min(const Sim& S, const MemSt& R, uint32_t 
     const uint32_t leaf = b * 64u + (uint32_t)S.lane;
     int64_t t = kInf;
     uint32_t s = 0xffffffffu, c = 0u;
+    if (PRISMA_BLK_UNIFORM && b * 64u + 64u <= R.L) {
+        // a block of links only (uniform): key and kind read together, no exec-mask branches
+        const uint2 k = R.lkey[leaf];
+        const uint32_t kind = R.lkind[leaf];
+        t = kind ? now + (int64_t)(uint32_t)(k.x - lo32(now)) : kInf;
+        s = kind ? k.y : 0xffffffffu;
+        c = (kind << 28) | leaf;
+        return wave_min_key(t, s, c, now);
+    }
     if (leaf < R.L) {
         const uint2 k = R.lkey[leaf];
         const uint32_t kind = R.lkind[leaf];
@@ -160,6 +179,38 @@ __device__ __forceinline__ Key block_min_cached(const Sim& S, const MemSt& R, ui
     return wave_min_key(t, s, c, now);
 }
 
+// the tree's top level (level 2): VGPRs (PRISMA_TOP_REG) or the LDS image
+__device__ __forceinline__ Key top_key(const MemSt& R, uint32_t g) {
+    if (PRISMA_TOP_REG) {
+        Key k;
+        k.t = mk64(rdl(R.g_tlo, g), rdl(R.g_thi, g));
+        k.s = rdl(R.g_s, g);
+        k.c = rdl(R.g_c, g);
+        return k;
+    }
+    return lds_key(&R.lv2[g]);
+}
+__device__ __forceinline__ void top_put(const Sim& S, MemSt& R, uint32_t g, const Key& k) {
+    if (PRISMA_TOP_REG) {
+        const bool me = (uint32_t)S.lane == g;
+        R.g_tlo = me ? lo32(k.t) : R.g_tlo;
+        R.g_thi = me ? hi32(k.t) : R.g_thi;
+        R.g_s = me ? k.s : R.g_s;
+        R.g_c = me ? k.c : R.g_c;
+        return;
+    }
+    lds_put_key(S, &R.lv2[g], k);
+}
+__device__ __forceinline__ void top_load(const Sim& S, MemSt& R) {
+    if (!PRISMA_TOP_REG) return;
+    const uint4 k = ((uint32_t)S.lane < R.n2) ? R.lv2[S.lane] : make_uint4(0xffffffffu, 0x7fffffffu, 0xffffffffu, 0u);
+    R.g_tlo = k.x; R.g_thi = k.y; R.g_s = k.z; R.g_c = k.w;
+}
+__device__ __forceinline__ void top_store(const Sim& S, const MemSt& R) {
+    if (!PRISMA_TOP_REG) return;
+    if ((uint32_t)S.lane < R.n2) R.lv2[S.lane] = make_uint4(R.g_tlo, R.g_thi, R.g_s, R.g_c);
+}
+
 // Source `leaf`'s next event changed to (t, seq): store its key and repair the two
 // tree levels above it.  A block is re-reduced only if the leaf was its minimum and
 // did not become smaller; a new smaller key just replaces it.
@@ -183,7 +234,7 @@ __device__ __forceinline__ void tree_touch(const Sim& S, MemSt& R, const Hot& H,
     }
     lds_put_key(S, &R.lv1[b], nb);
     const uint32_t g = b >> 6;
-    const Key cg = lds_key(&R.lv2[g]);
+    const Key cg = top_key(R, g);
     Key ng;
     if (key_less(nb.t, nb.s, cg.t, cg.s)) {
         ng = nb;
@@ -192,7 +243,7 @@ __device__ __forceinline__ void tree_touch(const Sim& S, MemSt& R, const Hot& H,
     } else {
         return;
     }
-    lds_put_key(S, &R.lv2[g], ng);
+    top_put(S, R, g, ng);
 }
 
 // ---- links: the whole record is one coalesced load (lane j: word j) and the fields
@@ -203,9 +254,9 @@ __device__ __forceinline__ uint32_t rec_load(const MemSt& R, uint32_t l) {
     return j < R.RW ? R.lrec[l * R.RW + j] : 0u;
 }
 
-__device__ __forceinline__ LinkV link_get(const MemSt& R, uint32_t l) {
+__device__ __forceinline__ LinkV link_fields(const MemSt& R, uint32_t rec) {
     LinkV k;
-    k.rec = rec_load(R, l);
+    k.rec = rec;
     const uint32_t p0 = rdl(k.rec, LR_P0), p1 = rdl(k.rec, LR_P1), p2 = rdl(k.rec, LR_P2);
     k.head = p0 & 0xffffu; k.txp = p0 >> 16;
     k.tail = p1 & 0xffffu; k.n_wire = p1 >> 16;
@@ -217,6 +268,7 @@ __device__ __forceinline__ LinkV link_get(const MemSt& R, uint32_t l) {
     k.wh_seq = rdl(k.rec, LR_WHS);
     return k;
 }
+__device__ __forceinline__ LinkV link_get(const MemSt& R, uint32_t l) { return link_fields(R, rec_load(R, l)); }
 
 template <unsigned MASK = LP_ALL>                 // (the whole record is written back either way)
 __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, uint32_t l, const LinkV& k) {
@@ -328,12 +380,40 @@ __device__ __forceinline__ uint32_t observe_links(const Sim& S, const MemSt& R, 
     return p[LR_QB];
 }
 
+// observe_links in two halves (PRISMA_OBS_EARLY): the gather's loads, unconditional (lanes outside
+// 1..deg read link 0 and discard it), then the per-lane value
+__device__ __forceinline__ ObsG obs_issue(const Sim& S, const MemSt& R, uint32_t v) {
+    const int r0 = t_ovrow(S, v), deg = t_ovrow(S, v + 1) - r0;
+    const int lane = S.lane;
+    const uint32_t li = (lane >= 1 && lane <= deg) ? (uint32_t)(r0 + lane - 1) : 0u;
+    const uint32_t* p = R.lrec + li * R.RW;
+    ObsG g;
+    if (S.lv.ping_as_obs()) {
+        g.a = p[LR_PAVLO]; g.b = p[LR_PAVHI]; g.c = p[LR_PMLO]; g.d = p[LR_ODLO]; g.e = p[LR_ODHI];
+    } else {
+        g.a = p[LR_QB]; g.b = 0u; g.c = 0u; g.d = 0u; g.e = 0u;
+    }
+    return g;
+}
+__device__ __forceinline__ uint32_t obs_finish(const Sim& S, const MemSt&, const Hot& H, uint32_t v, const ObsG& g,
+                                               double now_s) {
+    const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
+    const int lane = S.lane;
+    const uint32_t val = S.lv.ping_as_obs() ? ping_value_lane(ld_d(g.a, g.b), g.c, ld_d(g.d, g.e), H.ping_rounds, now_s)
+                                            : g.a;
+    return (lane >= 1 && lane <= deg) ? val : 0u;
+}
+
 // next event: minimum over the super-block minima and the ping timer
 __device__ __forceinline__ void select_event(const Sim& S, const MemSt& R, const Hot& H, int lane, int64_t& bt,
                                              uint32_t& bc, uint32_t& bs) {
     int64_t t = kInf;
     uint32_t s = 0xffffffffu, c = 0u;
-    if ((uint32_t)lane < R.n2) {
+    if (PRISMA_TOP_REG) {
+        t = mk64(R.g_tlo, R.g_thi);                                 // (lanes >= n2: infinite)
+        s = R.g_s;
+        c = R.g_c;
+    } else if ((uint32_t)lane < R.n2) {
         const uint4 k = R.lv2[lane];
         t = mk64(k.x, k.y);
         s = k.z;
@@ -391,6 +471,7 @@ __device__ __forceinline__ void mem_bind(Sim& S, MemSt& R, const KParams& P, con
     R.WCAP = (uint32_t)LC.WCAP;
     R.fblk = make_uint4(0u, 0u, 0u, 0u);
     R.fblk_b = ~0u;
+    R.g_tlo = 0xffffffffu; R.g_thi = 0x7fffffffu; R.g_s = 0xffffffffu; R.g_c = 0u;
 }
 
 // episode start (sim.cc:610-630, data-packet-manager.cc:118-121): LDS header,
@@ -519,7 +600,10 @@ __global__ void __launch_bounds__(64) prisma_mem_step_kernel(KParams P) {
 #ifndef PRISMA_MLP_B_MEM
 #define PRISMA_MLP_B_MEM kMlpAll
 #endif
+    top_load(S, R);
     event_loop<MLP, PRISMA_MLP_B_MEM>(P, S, R, r, (uint32_t)P.max_hops);
+    top_store(S, R);
+    __syncthreads();
     mem_stage(lds, P, r, lane, true);
 }
 

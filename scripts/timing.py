@@ -10,7 +10,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "prisma_amd", "_ablate", "libprisma_amd_timing.so")
+LIB = os.environ.get("PRISMA_TIMING_LIB", os.path.join(ROOT, "prisma_amd", "_ablate", "libprisma_amd_timing.so"))
 NAMES = ["select", "arrive", "decision", "complete", "flow", "ping_round", "dec:send", "dec:record"]
 
 if sys.argv[1] == "build":
@@ -26,7 +26,9 @@ if sys.argv[1] == "build":
             objs.append(os.path.join(ROOT, "prisma_amd", "csrc", os.path.splitext(f)[0] + ".o"))
             continue
         o = os.path.join(os.path.dirname(LIB), f + ".timing.o")
-        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", *buildid.HIPCC_FLAGS, "-DPRISMA_TIMING=1", "-c", "-o", o,
+        # PRISMA_TIMING_FLAGS: extra -D flags (the timing build of a variant)
+        extra = os.environ.get("PRISMA_TIMING_FLAGS", "").split()
+        procs.append(subprocess.Popen(["/opt/rocm/bin/hipcc", *buildid.HIPCC_FLAGS, *extra, "-DPRISMA_TIMING=1", "-c", "-o", o,
                                        os.path.join(ROOT, "prisma_amd", "csrc", f)]))
         objs.append(o)
     if any(p.wait() != 0 for p in procs):
@@ -93,9 +95,12 @@ if buf[20]:
     for i, nm in enumerate(["flow:record+block", "flow:send", "flow:draw", "flow:tree"]):
         print(f"  {nm:17s} cyc/flow={buf[20 + i] / max(1, nf):8.0f}")
 # fine probes TP(i) (engine_core.h): cycles since the previous probe, per execution
-PROBES = ["mlp:wait-arrival", "mlp:sum", "mlp:w3-issue", "mlp:var", "mlp:w4-issue", "mlp:den+xn",
+PROBES = (["arr:record", "arr:issue-prev+obs", "arr:wire-pop+tree", "arr:prev-wait", "arr:data-rest",
+           "arr:ctl-pop", "arr:ctl-rest", "cmp:record", "cmp:ring", "cmp:transmit", "cmp:put+tree",
+           "p11", "p12", "p13", "p14", "p15"] if os.environ.get("PRISMA_TP_SET") == "1" else
+          ["mlp:wait-arrival", "mlp:sum", "mlp:w3-issue", "mlp:var", "mlp:w4-issue", "mlp:den+xn",
           "mlp:l1-chunks", "mlp:l1-elu+store", "mlp:l2", "mlp:l3", "mlp:l4", "mlp:argmin",
-          "dec:send", "dec:record+cnt", "probe14", "probe15"]
+          "dec:send", "dec:record+cnt", "probe14", "probe15"])
 for i, nm in enumerate(PROBES):
     n = buf[40 + i]
     if n:
