@@ -725,6 +725,19 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
     if (k.n_wire > (uint32_t)L.WCAP()) fail(H, PRISMA_EBIT_WIRE);
 }
 
+// Whether a send must store its packet in the link's FIFO ring.  Tunnelled overlays and the
+// memory-resident engine keep the packets on a wire in wire slots (LDS / the link record), so a
+// packet that finds the transmitter idle and nothing queued goes straight onto the wire and its
+// ring slot is never read (PRISMA_RING_DIRECT): the store -- an HBM write there -- is skipped.  The
+// register-resident identity overlays read arrivals from the ring and always store.
+#ifndef PRISMA_RING_DIRECT
+#define PRISMA_RING_DIRECT 0
+#endif
+__device__ __forceinline__ bool ring_store_needed(const Sim& S, const LinkV& k) {
+    if (PRISMA_RING_DIRECT && (S.tun || S.mem)) return k.busy || k.n_queue != 0u;
+    return true;
+}
+
 // returns 1 if enqueued, 0 if dropped (a ring overflow fails the replica)
 // link_send with the link's state already fetched (the memory-resident engine's flow event
 // issues the record load early); the register-resident engine keeps the plain form below,
@@ -744,7 +757,7 @@ __device__ __forceinline__ int link_send_k(const Sim& S, RS& R, Hot& H, uint32_t
     }
     uint32_t cap = ring_cap(S, l), off = ring_off(S, l);
     if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
-    ring_put(S, off + k.tail, e);
+    if (ring_store_needed(S, k)) ring_put(S, off + k.tail, e);
     k.tail = (k.tail + 1 == cap) ? 0 : k.tail + 1;
     k.n_queue++;
     k.qb += size;
@@ -783,7 +796,7 @@ __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l
     }
     uint32_t cap = ring_cap(S, l), off = ring_off(S, l);
     if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
-    ring_put(S, off + k.tail, e);
+    if (ring_store_needed(S, k)) ring_put(S, off + k.tail, e);
     k.tail = (k.tail + 1 == cap) ? 0 : k.tail + 1;
     k.n_queue++;
     k.qb += size;
@@ -1551,7 +1564,8 @@ __device__ __forceinline__ float lds_sum_ordered(const float4* hb4, int nck) {
 }
 // a / d for an integer d (the node's degree) with rd = RN(1/d): q = a rd and one FMA correction
 // (Markstein), the correctly rounded quotient for 2^-120 <= a (and a = 0) and 1 <= d <= 64 --
-// checked exhaustively over every float a in that range (tests/test_numerics_division.py)
+// checked exhaustively over every float a in that range (scripts/checks/div_deg_exhaustive.c; a
+// sample in tests/test_numerics_division.py)
 __device__ __forceinline__ float div_deg(float a, float d, float rd) {
     const float q = __fmul_rn(a, rd);
     const float e = __builtin_fmaf(-q, d, a);

@@ -534,7 +534,15 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
     if (L.s_hdr != kOffHdr || L.s_cnt != kOffCnt || L.s_obs != kOffObs)
         return set_err(PRISMA_ERR_CONFIG, "internal: LDS header offsets");
     L.s_lv1 = take(16u * L.n1);
-    L.s_lv2 = take(16u * L.n2);
+    // level 2 / the top level: 64 entries (PRISMA_LINK_TOP: the link blocks and the flow groups)
+    L.s_lv2 = take(16u * 64u);
+#if PRISMA_LINK_TOP
+    {
+        const uint64_t n_lb = ((uint64_t)Lk + 63u) / 64u, n_fg = (((uint64_t)FG + 63u) / 64u + 63u) / 64u;
+        if (n_lb + n_fg > 64u)
+            return set_err(PRISMA_ERR_CONFIG, "memory-resident engine: more than 64 link blocks + flow groups");
+    }
+#endif
     L.s_lkey = take(8u * (uint64_t)Lk);
     L.s_lkind = take((uint64_t)Lk);
     if (L.rng_mode) take(kRngBytes);                // ns-3 streams: the last kRngBytes (engine_core.h)

@@ -41,7 +41,19 @@ struct MemSt {
     // group g {t lo, t hi, seq, code}, loaded from the LDS image when a launch starts and written
     // back when it ends: selecting an event and repairing level 2 need no LDS round trip
     uint32_t g_tlo, g_thi, g_s, g_c;
+    uint32_t FG, n_lb, n_fb, n_top;  // PRISMA_LINK_TOP: flow sources, link blocks, flow blocks, top lanes in use
 };
+// PRISMA_LINK_TOP: the links' 64-leaf blocks report straight to the top level (two levels for
+// links, whose events are most of a hop's), the flows keep blocks (LDS level 1) and groups (top);
+// the top level holds the link blocks in lanes [0, n_lb) and the flow groups in lanes
+// [n_lb, n_lb + n_fg), in VGPRs (it implies PRISMA_TOP_REG); the host checks n_lb + n_fg <= 64
+#ifndef PRISMA_LINK_TOP
+#define PRISMA_LINK_TOP 0
+#endif
+#if PRISMA_LINK_TOP
+#undef PRISMA_TOP_REG
+#define PRISMA_TOP_REG 1
+#endif
 #ifndef PRISMA_TOP_REG
 #define PRISMA_TOP_REG 0
 #endif
@@ -203,12 +215,107 @@ __device__ __forceinline__ void top_put(const Sim& S, MemSt& R, uint32_t g, cons
 }
 __device__ __forceinline__ void top_load(const Sim& S, MemSt& R) {
     if (!PRISMA_TOP_REG) return;
-    const uint4 k = ((uint32_t)S.lane < R.n2) ? R.lv2[S.lane] : make_uint4(0xffffffffu, 0x7fffffffu, 0xffffffffu, 0u);
+    const uint32_t nt = PRISMA_LINK_TOP ? R.n_top : R.n2;
+    const uint4 k = ((uint32_t)S.lane < nt) ? R.lv2[S.lane] : make_uint4(0xffffffffu, 0x7fffffffu, 0xffffffffu, 0u);
     R.g_tlo = k.x; R.g_thi = k.y; R.g_s = k.z; R.g_c = k.w;
 }
 __device__ __forceinline__ void top_store(const Sim& S, const MemSt& R) {
     if (!PRISMA_TOP_REG) return;
-    if ((uint32_t)S.lane < R.n2) R.lv2[S.lane] = make_uint4(R.g_tlo, R.g_thi, R.g_s, R.g_c);
+    if ((uint32_t)S.lane < (PRISMA_LINK_TOP ? R.n_top : R.n2)) R.lv2[S.lane] = make_uint4(R.g_tlo, R.g_thi, R.g_s, R.g_c);
+}
+
+// ---- PRISMA_LINK_TOP tree: link blocks (LDS leaves) -> top; flow blocks (HBM leaves, LDS
+// level 1) -> flow groups -> top ----
+__device__ __forceinline__ Key lblock_min(const Sim& S, const MemSt& R, uint32_t b, int64_t now) {
+    const uint32_t l = b * 64u + (uint32_t)S.lane;
+    int64_t t = kInf;
+    uint32_t s = 0xffffffffu, kind = 0u;
+    if (l < R.L) {
+        const uint2 k = R.lkey[l];                                  // key and kind read together
+        kind = R.lkind[l];
+        t = kind ? now + (int64_t)(uint32_t)(k.x - lo32(now)) : kInf;
+        s = kind ? k.y : 0xffffffffu;
+    }
+    return wave_min_key(t, s, (kind << 28) | l, now);
+}
+__device__ __forceinline__ Key fblock_min(const Sim& S, const MemSt& R, uint32_t fb, int64_t now) {
+    const uint32_t f = fb * 64u + (uint32_t)S.lane;
+    int64_t t = kInf;
+    uint32_t s = 0xffffffffu;
+    if (f < R.FG) {
+        const uint4 k = R.fkeys[f];
+        t = mk64(k.x, k.y);
+        s = k.z;
+    }
+    return wave_min_key(t, s, (K_FLOW << 28) | f, now);
+}
+// the cached block of the running flow event (flow_draw), with flow f holding its new key
+__device__ __forceinline__ Key fblock_min_cached(const Sim& S, const MemSt& R, uint32_t fb, int64_t now, uint32_t f,
+                                                 int64_t nt, uint32_t ns) {
+    const uint32_t fi = fb * 64u + (uint32_t)S.lane;
+    int64_t t = kInf;
+    uint32_t s = 0xffffffffu;
+    if (fi == f) {
+        t = nt; s = ns;
+    } else if (fi < R.FG) {
+        t = mk64(R.fblk.x, R.fblk.y);
+        s = R.fblk.z;
+    }
+    return wave_min_key(t, s, (K_FLOW << 28) | fi, now);
+}
+__device__ __forceinline__ Key fgroup_min(const Sim& S, const MemSt& R, uint32_t g, int64_t now) {
+    const uint32_t i = g * 64u + (uint32_t)S.lane;
+    int64_t t = kInf;
+    uint32_t s = 0xffffffffu, c = 0u;
+    if (i < R.n_fb) {
+        const uint4 k = R.lv1[i];
+        t = mk64(k.x, k.y);
+        s = k.z;
+        c = k.w;
+    }
+    return wave_min_key(t, s, c, now);
+}
+__device__ __forceinline__ void tree_touch_link(const Sim& S, MemSt& R, const Hot& H, uint32_t l, int64_t t,
+                                                uint32_t seq, uint32_t code, uint32_t kind) {
+    R.lkey[l] = make_uint2(lo32(t), seq);                           // every lane: same address, same value
+    R.lkind[l] = (uint8_t)kind;
+    const uint32_t b = l >> 6;
+    const Key cur = top_key(R, b);
+    Key nb;
+    if (key_less(t, seq, cur.t, cur.s)) {
+        nb.t = t; nb.s = seq; nb.c = code;
+    } else if ((cur.c & 0x0fffffffu) == l) {
+        nb = lblock_min(S, R, b, H.now);
+    } else {
+        return;
+    }
+    top_put(S, R, b, nb);
+}
+__device__ __forceinline__ void tree_touch_flow(const Sim& S, MemSt& R, const Hot& H, uint32_t f, int64_t t,
+                                                uint32_t seq, uint32_t draw) {
+    st_rep(S, &R.fkeys[f], make_uint4(lo32(t), hi32(t), seq, draw));
+    const uint32_t fb = f >> 6;
+    const Key cur = lds_key(&R.lv1[fb]);
+    Key nb;
+    if (key_less(t, seq, cur.t, cur.s)) {
+        nb.t = t; nb.s = seq; nb.c = (K_FLOW << 28) | f;
+    } else if ((cur.c & 0x0fffffffu) == f) {
+        nb = (fb == R.fblk_b) ? fblock_min_cached(S, R, fb, H.now, f, t, seq) : fblock_min(S, R, fb, H.now);
+    } else {
+        return;
+    }
+    lds_put_key(S, &R.lv1[fb], nb);
+    const uint32_t g = fb >> 6, lane = R.n_lb + g;
+    const Key cg = top_key(R, lane);
+    Key ng;
+    if (key_less(nb.t, nb.s, cg.t, cg.s)) {
+        ng = nb;
+    } else if (((cg.c & 0x0fffffffu) >> 6) == fb) {
+        ng = fgroup_min(S, R, g, H.now);
+    } else {
+        return;
+    }
+    top_put(S, R, lane, ng);
 }
 
 // Source `leaf`'s next event changed to (t, seq): store its key and repair the two
@@ -216,6 +323,11 @@ __device__ __forceinline__ void top_store(const Sim& S, const MemSt& R) {
 // did not become smaller; a new smaller key just replaces it.
 __device__ __forceinline__ void tree_touch(const Sim& S, MemSt& R, const Hot& H, uint32_t leaf, int64_t t,
                                            uint32_t seq, uint32_t code, uint32_t aux) {
+    if (PRISMA_LINK_TOP) {
+        if (leaf < R.L) tree_touch_link(S, R, H, leaf, t, seq, code, aux);
+        else tree_touch_flow(S, R, H, leaf - R.L, t, seq, aux);
+        return;
+    }
     if (leaf < R.L) {
         R.lkey[leaf] = make_uint2(lo32(t), seq);              // every lane: same address, same value
         R.lkind[leaf] = (uint8_t)aux;
@@ -298,6 +410,12 @@ __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, u
 // ---- flows ----
 __device__ __forceinline__ void flow_min_refresh(const Sim&, MemSt&, const Hot&) {}   // the event tree keeps it
 __device__ __forceinline__ uint32_t flow_draw(const Sim& S, MemSt& R, uint32_t f) {
+    if (PRISMA_LINK_TOP) {                                          // flow blocks numbered from flow 0
+        const uint32_t fb = f >> 6, fi = fb * 64u + (uint32_t)S.lane;
+        R.fblk = fi < R.FG ? R.fkeys[fi] : make_uint4(0u, 0u, 0u, 0u);
+        R.fblk_b = fb;
+        return rdl(R.fblk.w, f & 63u);
+    }
     const uint32_t leaf = R.L + f, b = leaf >> 6, li = b * 64u + (uint32_t)S.lane;
     R.fblk = (li >= R.L && li < R.n_leaf) ? R.fkeys[li - R.L] : make_uint4(0u, 0u, 0u, 0u);
     R.fblk_b = b;
@@ -472,6 +590,10 @@ __device__ __forceinline__ void mem_bind(Sim& S, MemSt& R, const KParams& P, con
     R.fblk = make_uint4(0u, 0u, 0u, 0u);
     R.fblk_b = ~0u;
     R.g_tlo = 0xffffffffu; R.g_thi = 0x7fffffffu; R.g_s = 0xffffffffu; R.g_c = 0u;
+    R.FG = R.n_leaf - R.L;
+    R.n_lb = (R.L + 63u) / 64u;
+    R.n_fb = (R.FG + 63u) / 64u;
+    R.n_top = R.n_lb + (R.n_fb + 63u) / 64u;
 }
 
 // episode start (sim.cc:610-630, data-packet-manager.cc:118-121): LDS header,
@@ -523,9 +645,17 @@ __device__ __forceinline__ void init_replica(Sim& S, MemSt& R, Hot& H, uint32_t 
         R.fkeys[f] = make_uint4(lo32(t), hi32(t), S.m_fseq[f], 0u);
     }
     __syncthreads();
-    for (uint32_t b = 0; b < R.n1; ++b) lds_put_key(S, &R.lv1[b], block_min(S, R, b, 0));
-    __syncthreads();
-    for (uint32_t g = 0; g < R.n2; ++g) lds_put_key(S, &R.lv2[g], group_min(S, R, g, 0));
+    if (PRISMA_LINK_TOP) {
+        for (uint32_t b = 0; b < R.n_lb; ++b) top_put(S, R, b, lblock_min(S, R, b, 0));
+        for (uint32_t fb = 0; fb < R.n_fb; ++fb) lds_put_key(S, &R.lv1[fb], fblock_min(S, R, fb, 0));
+        __syncthreads();
+        for (uint32_t g = 0; R.n_lb + g < R.n_top; ++g) top_put(S, R, R.n_lb + g, fgroup_min(S, R, g, 0));
+        top_store(S, R);
+    } else {
+        for (uint32_t b = 0; b < R.n1; ++b) lds_put_key(S, &R.lv1[b], block_min(S, R, b, 0));
+        __syncthreads();
+        for (uint32_t g = 0; g < R.n2; ++g) lds_put_key(S, &R.lv2[g], group_min(S, R, g, 0));
+    }
     H.now = 0;
     H.ping_t = L.ping_period();
     H.ping_seq = 0;

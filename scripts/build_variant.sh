@@ -15,7 +15,8 @@ PIDS=()
 for f in $SRCS; do
   # ONLY=<source>: that translation unit alone, the others from the in-tree objects of the last
   # build_engine (same sources; quick memory-engine experiments)
-  if [ -n "$ONLY" ] && [ "$f" != "$ONLY" ]; then cp prisma_amd/csrc/${f%.hip}.o $O/; continue; fi
+  # (ONLY may list several translation units, space-separated)
+  if [ -n "$ONLY" ] && [[ " $ONLY " != *" $f "* ]]; then cp prisma_amd/csrc/${f%.hip}.o $O/; continue; fi
   /opt/rocm/bin/hipcc $FLAGS -DPRISMA_BUILD_ID="\"variant-$NAME\"" "$@" -c -o $O/${f%.hip}.o ${SRC_DIR:-prisma_amd/csrc}/$f &
   PIDS+=($!)
 done

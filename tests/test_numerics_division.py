@@ -43,3 +43,45 @@ def test_device_constant_division_equals_ieee_division():
         subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-o", exe, src, "-lm"])
         n, bad = map(int, subprocess.check_output([exe], text=True).split())
     assert n > 3e7 and bad == 0
+
+
+C_DEG = r'''
+#include <stdio.h>
+#include <stdint.h>
+#include <string.h>
+#include <math.h>
+/* engine_core.h div_deg: a / d for the node degree d with rd = RN(1/d) */
+static float div_deg(float a, float d, float rd) { float q = a * rd; float e = fmaf(-q, d, a); return fmaf(e, rd, q); }
+static uint64_t s = 0x9E3779B97F4A7C15ull;
+static uint64_t xr(void) { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return s; }
+int main(void) {
+    long bad = 0, n = 0;
+    for (int d = 1; d <= 64; ++d) {
+        const float fd = (float)d, rd = 1.0f / fd;
+        for (uint32_t u = 0x3f800000u; u < 0x40000000u; u += 7u) {      /* the binade [1, 2) */
+            float a; memcpy(&a, &u, 4); n++; if (div_deg(a, fd, rd) != a / fd) bad++;
+        }
+        for (int i = 0; i < 300000; ++i) {                              /* every exponent from 2^-120 */
+            uint32_t u = 0x03800000u + (uint32_t)(xr() % (0x7f800000u - 0x03800000u));
+            float a; memcpy(&a, &u, 4); n++; if (div_deg(a, fd, rd) != a / fd) bad++;
+        }
+        for (uint32_t k = 0; k < 400000; ++k) {                         /* integer sums (queued bytes) */
+            const float a = (float)k; n++; if (div_deg(a, fd, rd) != a / fd) bad++;
+        }
+    }
+    printf("%ld %ld\n", n, bad);
+    return 0;
+}
+'''
+
+
+def test_degree_division_equals_ieee_division():
+    """engine_core.h div_deg (the memory-resident LayerNorm's mean and variance over the node degree):
+    the Markstein correction with RN(1/d) equals IEEE float division for d = 1..64 on a sample here;
+    scripts/checks/div_deg_exhaustive.c checks every float >= 2^-120 (0 mismatches)."""
+    with tempfile.TemporaryDirectory() as d:
+        src, exe = os.path.join(d, "deg.c"), os.path.join(d, "deg")
+        open(src, "w").write(C_DEG)
+        subprocess.check_call(["gcc", "-O2", "-ffp-contract=off", "-o", exe, src, "-lm"])
+        n, bad = map(int, subprocess.check_output([exe], text=True).split())
+    assert n > 1e8 and bad == 0
