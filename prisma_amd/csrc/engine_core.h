@@ -505,10 +505,6 @@ __device__ __forceinline__ uint32_t ring_cap(const Sim& S, uint32_t l) {
 }
 
 // one link's fields as uniform scalars
-// an observation gather in flight (memory-resident engine, PRISMA_OBS_EARLY): the link-record
-// words of lane i's out-link (queued bytes, or the ping words)
-struct ObsG { uint32_t a, b, c, d, e; };
-
 struct LinkV {
     uint32_t head, txp, tail, n_wire, n_queue, busy, qb;
     uint32_t cp_t, cp_seq;       // completion time (low 32 bits), seq
@@ -731,7 +727,7 @@ __device__ __forceinline__ void transmit_start(const Sim& S, Hot& H, uint32_t l,
 // ring slot is never read (PRISMA_RING_DIRECT): the store -- an HBM write there -- is skipped.  The
 // register-resident identity overlays read arrivals from the ring and always store.
 #ifndef PRISMA_RING_DIRECT
-#define PRISMA_RING_DIRECT 0
+#define PRISMA_RING_DIRECT 1
 #endif
 __device__ __forceinline__ bool ring_store_needed(const Sim& S, const LinkV& k) {
     if (PRISMA_RING_DIRECT && (S.tun || S.mem)) return k.busy || k.n_queue != 0u;
@@ -900,22 +896,6 @@ __device__ __forceinline__ uint32_t observe_links(const Sim& S, const Regs<FS, L
     return (lane >= 1 && lane <= deg) ? o : 0u;
 }
 
-#ifndef PRISMA_NT_LOG
-#define PRISMA_NT_LOG 0
-#endif
-#ifndef PRISMA_NT_PREV
-#define PRISMA_NT_PREV 0
-#endif
-typedef unsigned int nt_u32x4 __attribute__((ext_vector_type(4)));
-typedef unsigned int nt_u32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint4 ld_nt4(const void* p) {
-    const nt_u32x4 v = __builtin_nontemporal_load((const nt_u32x4*)p);
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
-__device__ __forceinline__ uint2 ld_nt2(const void* p) {
-    const nt_u32x2 v = __builtin_nontemporal_load((const nt_u32x2*)p);
-    return make_uint2(v.x, v.y);
-}
 // one coalesced wave store of a decision record (lane i writes word i)
 __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_t d, double reward, uint32_t uid,
                                              int32_t prev, uint32_t node, uint32_t dst, uint32_t start, int action,
@@ -939,12 +919,7 @@ __device__ __forceinline__ void write_record(const Sim& S, const Hot& H, uint32_
     uint32_t ob = bperm(obs_reg, (uint32_t)(lane - 8) & 63u);
     uint32_t word = bfi(S.m8, hw, ob);
     uint32_t* p = (uint32_t*)(S.logrep + (size_t)(d & (S.lv.log_cap() - 1)) * S.lv.rec_bytes());
-    if (lane < 8 + S.lv.W()) {
-        // PRISMA_NT_LOG: the log is streamed out (read back once, long after): a non-temporal
-        // store keeps it from displacing the replica state in the caches
-        if (PRISMA_NT_LOG) __builtin_nontemporal_store(word, p + lane);
-        else p[lane] = word;
-    }
+    if (lane < 8 + S.lv.W()) p[lane] = word;
 }
 
 // action + status of a record written earlier (TTL and episode bytes kept)
@@ -1346,23 +1321,6 @@ __device__ __forceinline__ void mlp_preload_w4(MlpPre& M, const float* __restric
 #ifndef PRISMA_PRE_W2
 #define PRISMA_PRE_W2 0
 #endif
-#ifndef PRISMA_OBS_EARLY
-#define PRISMA_OBS_EARLY 0
-#endif
-#ifndef PRISMA_PRE_AFTER_OBS
-#define PRISMA_PRE_AFTER_OBS 0
-#endif
-#ifndef PRISMA_MLP_CHAINS
-#define PRISMA_MLP_CHAINS 1
-#endif
-// where the memory-resident engine issues layer 3's / layer 4's weights: 0 inside the LayerNorm
-// (after its first / second sum), 1 when layer 1 ends, 2 (layer 4 only) when layer 2 ends
-#ifndef PRISMA_W3_AT
-#define PRISMA_W3_AT 0
-#endif
-#ifndef PRISMA_W4_AT
-#define PRISMA_W4_AT 0
-#endif
 __device__ __forceinline__ void mlp_preload_node(MlpPre1& M, const Sim& S, uint32_t v, uint32_t dst, bool has_w1) {
     const int lane = S.lane;
     v = rfl(v);                  // uniform: the row pointers come from scalar loads
@@ -1387,22 +1345,6 @@ __device__ __forceinline__ void mlp_preload_node(MlpPre1& M, const Sim& S, uint3
 
 __device__ __forceinline__ float mlp_dense64_pre(const Sim& S, const float4 (&w)[16], float b) {
     const float4* __restrict__ hb = (const float4*)S.hbuf;
-    if (PRISMA_MLP_CHAINS == 2) {            // (perf experiment: two chains, even / odd chunks)
-        float a0 = 0.0f, a1 = 0.0f;
-#pragma unroll
-        for (int c = 0; c < 16; c += 2) {
-            const float4 h0 = hb[c], h1 = hb[c + 1];
-            a0 = __builtin_fmaf(h0.x, w[c].x, a0);
-            a1 = __builtin_fmaf(h1.x, w[c + 1].x, a1);
-            a0 = __builtin_fmaf(h0.y, w[c].y, a0);
-            a1 = __builtin_fmaf(h1.y, w[c + 1].y, a1);
-            a0 = __builtin_fmaf(h0.z, w[c].z, a0);
-            a1 = __builtin_fmaf(h1.z, w[c + 1].z, a1);
-            a0 = __builtin_fmaf(h0.w, w[c].w, a0);
-            a1 = __builtin_fmaf(h1.w, w[c + 1].w, a1);
-        }
-        return __fadd_rn(__fadd_rn(a0, a1), b);
-    }
     float acc = 0.0f;
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
@@ -1543,9 +1485,6 @@ __device__ __forceinline__ int lane_argmin_first(float q, int n) {
 #ifndef PRISMA_LN_LDS
 #define PRISMA_LN_LDS 1
 #endif
-#ifndef PRISMA_LN_LDS_REG
-#define PRISMA_LN_LDS_REG 0
-#endif
 __device__ __forceinline__ float lds_sum_ordered(const float4* hb4, int nck) {
     float4 h[8];
 #pragma unroll
@@ -1654,8 +1593,8 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     // (the memory-resident engine's single wave per SIMD gains from the 4-wide sums and the
     // DPP argmin below; the register-resident MLP instances lost 1 % with them, A/B on GEANT)
     const float xf = (float)obs_reg;
-    // (PRISMA_LN_LDS_REG: the register-resident instances too)
-    constexpr bool kLnLds = (B == kMlpAll || PRISMA_LN_LDS_REG) && PRISMA_LN_LDS;
+    // (the register-resident instances lost 0.5-1.2 % with it at 4 waves per SIMD, round-5 A/B)
+    constexpr bool kLnLds = (B == kMlpAll) && PRISMA_LN_LDS;
     const float4* hb4 = (const float4*)S.hbuf;
     const bool inb = lane >= 1 && lane <= deg;
     const float fdeg = (float)deg;
@@ -1669,7 +1608,7 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     } else if constexpr (B == kMlpAll) sum = lane_sum_ordered(xf, deg);
     else for (int k = 0; k < deg; ++k) sum = __fadd_rn(sum, rdlf(xf, (uint32_t)(k + 1)));
     TP0(1);
-    if constexpr (B == kMlpAll && PRE && PRISMA_W3_AT == 0) {
+    if constexpr (B == kMlpAll && PRE) {
         __builtin_amdgcn_sched_barrier(0);
         mlp_preload_w3(M, RP, lane);
         __builtin_amdgcn_sched_barrier(0);
@@ -1687,7 +1626,7 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     } else if constexpr (B == kMlpAll) var = lane_sum_ordered(sq, deg);
     else for (int k = 0; k < deg; ++k) var = __fadd_rn(var, rdlf(sq, (uint32_t)(k + 1)));
     TP0(3);
-    if constexpr (B == kMlpAll && PRE && PRISMA_W4_AT == 0) {
+    if constexpr (B == kMlpAll && PRE) {
         __builtin_amdgcn_sched_barrier(0);
         mlp_preload_w4(M, RP, lane, D, deg);
         __builtin_amdgcn_sched_barrier(0);
@@ -1755,16 +1694,6 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     __builtin_amdgcn_wave_barrier();
     TP0(7);
     TM_MLP(0);
-    if constexpr (B == kMlpAll && PRE && PRISMA_W3_AT == 1) {
-        __builtin_amdgcn_sched_barrier(0);
-        mlp_preload_w3(M, RP, lane);
-        __builtin_amdgcn_sched_barrier(0);
-    }
-    if constexpr (B == kMlpAll && PRE && PRISMA_W4_AT == 1) {
-        __builtin_amdgcn_sched_barrier(0);
-        mlp_preload_w4(M, RP, lane, D, deg);
-        __builtin_amdgcn_sched_barrier(0);
-    }
     if constexpr (B != kMlpAll && PRISMA_MLP_PIPE) {
         // (half batches double-buffered: the same weight registers as B loads in flight)
         const float q4 = mlp_l234_pipe<kPipeB, kPipeEarly>(S, RP, lane, D, deg, w20);
@@ -1780,11 +1709,6 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     __builtin_amdgcn_wave_barrier();
     TP0(8);
     TM_MLP(1);
-    if constexpr (B == kMlpAll && PRE && PRISMA_W4_AT == 2) {
-        __builtin_amdgcn_sched_barrier(0);
-        mlp_preload_w4(M, RP, lane, D, deg);
-        __builtin_amdgcn_sched_barrier(0);
-    }
     if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w3, M.b3));
     else h = det_elu(mlp_dense64<B>(S, RP + mlp_rp_layer_floats(64), lane, 64));
     __builtin_amdgcn_wave_barrier();
@@ -1905,19 +1829,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
     const LV& L = S.lv;
     if (S.mem) TP1_START();
     const uint32_t v = (uint32_t)t_ldst(S, l);
-    // memory-resident engine (PRISMA_OBS_EARLY): node v's observation is gathered before the
-    // arrival link's record comes back -- it depends on v alone, and nothing this arrival does
-    // before a decision writes v's out-links -- so its round trip overlaps the record's; the
-    // arrivals that decide nothing (pings, packets at their destination) discard it
-    ObsG og;
-    LinkV k;
-    if constexpr (RS::kMem && PRISMA_OBS_EARLY) {
-        const uint32_t rec = rec_load(R, l);                        // issued first ...
-        og = obs_issue(S, R, v);                                    // ... the gather behind it
-        k = link_fields(R, rec);                                    // waits for the record only
-    } else {
-        k = link_get(R, l);
-    }
+    LinkV k = link_get(R, l);
     const uint32_t wh = k.head & (uint32_t)(L.WCAP() - 1);
     const uint32_t x = S.mem ? wire_ent(S, k, wh)
                              : (S.tun ? u_ld32(&S.went[l * (uint32_t)L.WCAP() + wh])
@@ -1938,9 +1850,9 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         const uint32_t d = H.dec;
         const uint32_t dist = (d - r_dec(x)) & kRelayMask;
         const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap() - 1)) * L.rec_bytes();
-        const uint4 ph = PRISMA_NT_PREV ? ld_nt4(pr) : *(const uint4*)pr;
-        const uint2 pw = PRISMA_NT_PREV ? ld_nt2(pr + 24) : *(const uint2*)(pr + 24);
-        if (PRE && !PRISMA_PRE_AFTER_OBS) {                         // the decision's weights ride along
+        const uint4 ph = *(const uint4*)pr;
+        const uint2 pw = *(const uint2*)(pr + 24);
+        if constexpr (PRE) {                                        // the decision's weights ride along
             if (S.ctrl) {
                 mlp_preload_node(Mpre, S, v, 0u, false);
             } else {
@@ -1953,17 +1865,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         // memory-resident engine: the observation's gather goes out with the record
         // load, before the arrival link's update (it reads node v's out-links, which
         // nothing touches before the decision)
-        uint32_t obs_early = 0u;
-        if constexpr (RS::kMem && PRISMA_OBS_EARLY) obs_early = obs_finish(S, R, H, v, og, ns_to_sec(H.now));
-        else if (S.mem) obs_early = observe_links(S, R, H, v, ns_to_sec(H.now));
-        if (PRE && PRISMA_PRE_AFTER_OBS) {          // (issued behind the gather: the arrival does not wait for them)
-            if (S.ctrl) {
-                mlp_preload_node(Mpre, S, v, 0u, false);
-            } else {
-                const uint32_t dst_e = (type == T_FRESH) ? f_dst(x) : r_dst(x);
-                if (dst_e != v) mlp_preload_node(Mpre, S, v, dst_e, true);
-            }
-        }
+        const uint32_t obs_early = S.mem ? observe_links(S, R, H, v, ns_to_sec(H.now)) : 0u;
         if (S.mem) TP1(1);
         wire_pop(S, R, H, l, k);
         if (S.mem) TP1(2);

@@ -188,8 +188,8 @@ struct Layout {
     // the header, counters, pending obs and the upper levels of the event tree;
     // s_ring / s_win / s_pbd are offsets into the HBM part of the state image.
     uint32_t mem;
-    uint32_t n_leaf, n1, n2;     // event tree: leaves (links, then flows), level-1 / level-2 nodes
-    uint32_t s_lv1, s_lv2;       // LDS offsets of the tree levels (16-B nodes)
+    uint32_t n_leaf, n1, n2;     // event tree: sources (links + flow slots), flow blocks, top-level entries
+    uint32_t s_lv1, s_lv2;       // LDS offsets of the flow block minima and the top level's image (16-B nodes)
     uint32_t g_lrec, g_keys;     // image offsets of the link records and the flow leaf keys
     uint32_t lrec_words;         // words per link record (32 or 64)
     uint32_t s_lkey, s_lkind;    // LDS offsets of the link leaf keys (time lo, seq) and kinds (bytes)

@@ -492,8 +492,13 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
     if (n_leaf > 64ull * 64ull * 64ull) return set_err(PRISMA_ERR_CONFIG, "more than 262 144 links + flows per replica");
     L.mem = 1;
     L.n_leaf = (uint32_t)n_leaf;
-    L.n1 = (L.n_leaf + 63u) / 64u;
-    L.n2 = (L.n1 + 63u) / 64u;
+    // event tree (prisma_engine_mem.hip): link blocks report to the top level, flow blocks (n1)
+    // to flow groups there; the top level is one VGPR per lane: at most 64 entries
+    L.n1 = (FG + 63u) / 64u;
+    L.n2 = ((uint32_t)Lk + 63u) / 64u + (L.n1 + 63u) / 64u;
+    if (L.n2 > 64u)
+        return set_err(PRISMA_ERR_CONFIG, "memory-resident engine: more than 64 link blocks + flow groups "
+                                          "(about 3 000 links at 65 000 flows)");
     uint64_t o = 0;
     auto take = [&](uint64_t bytes) { uint64_t r = o; o = (o + bytes + 15u) & ~(uint64_t)15u; return (uint32_t)r; };
     L.t_rowptr = take(4u * (N + 1));
@@ -533,16 +538,8 @@ static int layout_mem(const prisma_topology_t* T, const prisma_params_t* P, Layo
     L.s_obs = take(4u * L.W);
     if (L.s_hdr != kOffHdr || L.s_cnt != kOffCnt || L.s_obs != kOffObs)
         return set_err(PRISMA_ERR_CONFIG, "internal: LDS header offsets");
-    L.s_lv1 = take(16u * L.n1);
-    // level 2 / the top level: 64 entries (PRISMA_LINK_TOP: the link blocks and the flow groups)
-    L.s_lv2 = take(16u * 64u);
-#if PRISMA_LINK_TOP
-    {
-        const uint64_t n_lb = ((uint64_t)Lk + 63u) / 64u, n_fg = (((uint64_t)FG + 63u) / 64u + 63u) / 64u;
-        if (n_lb + n_fg > 64u)
-            return set_err(PRISMA_ERR_CONFIG, "memory-resident engine: more than 64 link blocks + flow groups");
-    }
-#endif
+    L.s_lv1 = take(16u * L.n1);                      // flow block minima
+    L.s_lv2 = take(16u * L.n2);                      // the top level's image between launches
     L.s_lkey = take(8u * (uint64_t)Lk);
     L.s_lkind = take((uint64_t)Lk);
     if (L.rng_mode) take(kRngBytes);                // ns-3 streams: the last kRngBytes (engine_core.h)

@@ -1,19 +1,21 @@
 // prisma_engine_mem.hip — the memory-resident gfx950 engine.
 //
 // For topologies beyond the register-resident engine (more than 255 nodes,
-// 256 links or 512 flows: the Erdos-Renyi 256-node config, 2 304 links and
-// 65 280 flows per replica) the replica state lives in HBM and one 64-lane
+// 256 links or 512 flows: the Erdos-Renyi 256-node config, 2 264 links and
+// 65 251 flows per replica) the replica state lives in HBM and one 64-lane
 // wavefront still owns one replica and runs the same event handlers
 // (engine_core.h), over a different store (MemSt):
 //   * one 128-byte record per link (FIFO pointers, queued bytes, completion and
-//     wire-head keys, ping state of the link's tunnel, 8 wire slots), read and
-//     written by every lane as uniform 16-B accesses;
-//   * the next event of every source (links, then flows) as a 16-byte leaf key
-//     {time lo, time hi, seq, aux} in HBM, under a 64-ary tournament tree whose
-//     two upper levels (block and super-block minima) sit in LDS.  A source's
-//     update re-reduces its 64-leaf block (one coalesced 1 KiB load + a DPP
-//     reduction) only when the block minimum can change, and the level above
-//     likewise; choosing the next event reduces <= 64 super-block minima;
+//     wire-head keys, ping state of the link's tunnel, the wire slots), read and
+//     written as one coalesced wave access (lane j: word j);
+//   * the next event of every source under a 64-ary tournament tree (round 5): link
+//     leaves {time lo, seq} + kind in LDS, whose 64-leaf blocks report straight to the
+//     top level; flow leaves {time lo, time hi, seq, draw} in HBM, under flow blocks (LDS)
+//     and flow groups; the top level -- the link blocks in lanes [0, n_lb), the flow groups
+//     in lanes [n_lb, n_top) -- sits in four VGPRs (its LDS image carries it from launch to
+//     launch).  A source's update re-reduces its block (one LDS read or one coalesced 1 KiB
+//     HBM read + a DPP reduction) only when the block minimum can change, and a flow block's
+//     group likewise; choosing the next event is one reduction of the top lanes;
 //   * FIFO rings, ping windows and ping-back delays in HBM (ring offsets as in
 //     the register-resident engine).
 // The header, counters and pending observation stay in LDS (staged per launch).
@@ -26,46 +28,25 @@ struct MemSt {
     static constexpr bool kLazy = true;          // empty-queue transmit completions elided (lazy_resolve)
     static constexpr bool kMem = true;
     uint32_t* lrec;              // [L][RW] link records (HBM)
-    uint4* fkeys;                // [F] flow leaf keys {t lo, t hi, seq, draw} (HBM)
+    uint4* fkeys;                // [FG] flow leaf keys {t lo, t hi, seq, draw} (HBM)
     uint2* lkey;                 // LDS [L] link leaf keys {t lo, seq}: t = now + (t lo - lo32(now))
     uint8_t* lkind;              // LDS [L] link event kind (0: none, K_COMPLETE, K_ARRIVE)
-    uint4* lv1;                  // LDS [n1] {t lo, t hi, seq, code}
-    uint4* lv2;                  // LDS [n2]
-    uint32_t L, n_leaf, n1, n2, RW, WCAP;
+    uint4* fblkmin;              // LDS [n_fb] flow block minima {t lo, t hi, seq, code}
+    uint4* topimg;               // LDS [64] the top level's image between launches
+    uint32_t L, FG, n_lb, n_fb, n_top, RW, WCAP;
     // the 64-leaf block of the flow whose send event runs, loaded (one coalesced 1 KiB
     // load) by flow_draw for its draw index; flow_set re-reduces the block from it instead
     // of storing the new key and loading the block back (one HBM round trip per flow event)
     uint4 fblk;
     uint32_t fblk_b;             // its block index, or ~0u
-    // PRISMA_TOP_REG: the tree's top level (level 2, n2 <= 64 group minima) in VGPRs, lane g =
-    // group g {t lo, t hi, seq, code}, loaded from the LDS image when a launch starts and written
-    // back when it ends: selecting an event and repairing level 2 need no LDS round trip
+    // the top level, lane i = entry i {t lo, t hi, seq, code}: link block i (i < n_lb) or flow
+    // group i - n_lb (i < n_top); infinite past n_top.  A link event -- most of a hop's events --
+    // repairs its block and one top lane, with no LDS round trip at the top and no group level
+    // (round 5, A/B on one box: config 5 DQN-buffer 89.1 -> 95.6 Mhops/s, SP table 111 -> 121)
     uint32_t g_tlo, g_thi, g_s, g_c;
-    uint32_t FG, n_lb, n_fb, n_top;  // PRISMA_LINK_TOP: flow sources, link blocks, flow blocks, top lanes in use
 };
-// PRISMA_LINK_TOP: the links' 64-leaf blocks report straight to the top level (two levels for
-// links, whose events are most of a hop's), the flows keep blocks (LDS level 1) and groups (top);
-// the top level holds the link blocks in lanes [0, n_lb) and the flow groups in lanes
-// [n_lb, n_lb + n_fg), in VGPRs (it implies PRISMA_TOP_REG); the host checks n_lb + n_fg <= 64
-#ifndef PRISMA_LINK_TOP
-#define PRISMA_LINK_TOP 0
-#endif
-#if PRISMA_LINK_TOP
-#undef PRISMA_TOP_REG
-#define PRISMA_TOP_REG 1
-#endif
-#ifndef PRISMA_TOP_REG
-#define PRISMA_TOP_REG 0
-#endif
-#ifndef PRISMA_BLK_UNIFORM
-#define PRISMA_BLK_UNIFORM 0
-#endif
 
 constexpr int64_t kInf = INT64_MAX;
-
-__device__ __forceinline__ uint32_t leaf_of(const MemSt& R, uint32_t code) {
-    return (code >> 28) == K_FLOW ? R.L + (code & 0x0fffffffu) : (code & 0x0fffffffu);
-}
 
 // uniform (t, seq, code) minimum over the lanes (lowest (t, seq); seqs are unique
 // among finite keys, so the winner is unique unless every key is infinite)
@@ -122,110 +103,31 @@ __device__ __forceinline__ void lds_put_key(const Sim& S, uint4* p, const Key& k
     *p = make_uint4(lo32(k.t), hi32(k.t), k.s, k.c);     // every lane: same address, same value
 }
 
-// minimum of leaf block b (64 leaves, one per lane): links from LDS, flows from HBM
-__device__ __forceinline__ Key block_min(const Sim& S, const MemSt& R, uint32_t b, int64_t now) {
-    const uint32_t leaf = b * 64u + (uint32_t)S.lane;
-    int64_t t = kInf;
-    uint32_t s = 0xffffffffu, c = 0u;
-    if (PRISMA_BLK_UNIFORM && b * 64u + 64u <= R.L) {
-        // a block of links only (uniform): key and kind read together, no exec-mask branches
-        const uint2 k = R.lkey[leaf];
-        const uint32_t kind = R.lkind[leaf];
-        t = kind ? now + (int64_t)(uint32_t)(k.x - lo32(now)) : kInf;
-        s = kind ? k.y : 0xffffffffu;
-        c = (kind << 28) | leaf;
-        return wave_min_key(t, s, c, now);
-    }
-    if (leaf < R.L) {
-        const uint2 k = R.lkey[leaf];
-        const uint32_t kind = R.lkind[leaf];
-        if (kind) {
-            t = now + (int64_t)(uint32_t)(k.x - lo32(now));
-            s = k.y;
-        }
-        c = (kind << 28) | leaf;
-    } else if (leaf < R.n_leaf) {
-        const uint4 k = R.fkeys[leaf - R.L];
-        t = mk64(k.x, k.y);
-        s = k.z;
-        c = (K_FLOW << 28) | (leaf - R.L);
-    }
-    return wave_min_key(t, s, c, now);
+// ---- the top level (VGPRs) ----
+__device__ __forceinline__ Key top_key(const MemSt& R, uint32_t i) {
+    Key k;
+    k.t = mk64(rdl(R.g_tlo, i), rdl(R.g_thi, i));
+    k.s = rdl(R.g_s, i);
+    k.c = rdl(R.g_c, i);
+    return k;
 }
-// minimum of level-1 group g (64 block minima)
-__device__ __forceinline__ Key group_min(const Sim& S, const MemSt& R, uint32_t g, int64_t now) {
-    const uint32_t i = g * 64u + (uint32_t)S.lane;
-    int64_t t = kInf;
-    uint32_t s = 0xffffffffu, c = 0u;
-    if (i < R.n1) {
-        const uint4 k = R.lv1[i];
-        t = mk64(k.x, k.y);
-        s = k.z;
-        c = k.w;
-    }
-    return wave_min_key(t, s, c, now);
-}
-
-// block_min of the cached flow block, with `leaf` holding the new key (t, seq, code); link
-// leaves of the block (the one straddling links and flows) are read from LDS as usual
-__device__ __forceinline__ Key block_min_cached(const Sim& S, const MemSt& R, uint32_t b, int64_t now, uint32_t leaf,
-                                                int64_t nt, uint32_t ns, uint32_t ncode) {
-    const uint32_t li = b * 64u + (uint32_t)S.lane;
-    int64_t t = kInf;
-    uint32_t s = 0xffffffffu, c = 0u;
-    if (li < R.L) {
-        const uint2 k = R.lkey[li];
-        const uint32_t kind = R.lkind[li];
-        if (kind) {
-            t = now + (int64_t)(uint32_t)(k.x - lo32(now));
-            s = k.y;
-        }
-        c = (kind << 28) | li;
-    } else if (li == leaf) {
-        t = nt; s = ns; c = ncode;
-    } else if (li < R.n_leaf) {
-        t = mk64(R.fblk.x, R.fblk.y);
-        s = R.fblk.z;
-        c = (K_FLOW << 28) | (li - R.L);
-    }
-    return wave_min_key(t, s, c, now);
-}
-
-// the tree's top level (level 2): VGPRs (PRISMA_TOP_REG) or the LDS image
-__device__ __forceinline__ Key top_key(const MemSt& R, uint32_t g) {
-    if (PRISMA_TOP_REG) {
-        Key k;
-        k.t = mk64(rdl(R.g_tlo, g), rdl(R.g_thi, g));
-        k.s = rdl(R.g_s, g);
-        k.c = rdl(R.g_c, g);
-        return k;
-    }
-    return lds_key(&R.lv2[g]);
-}
-__device__ __forceinline__ void top_put(const Sim& S, MemSt& R, uint32_t g, const Key& k) {
-    if (PRISMA_TOP_REG) {
-        const bool me = (uint32_t)S.lane == g;
-        R.g_tlo = me ? lo32(k.t) : R.g_tlo;
-        R.g_thi = me ? hi32(k.t) : R.g_thi;
-        R.g_s = me ? k.s : R.g_s;
-        R.g_c = me ? k.c : R.g_c;
-        return;
-    }
-    lds_put_key(S, &R.lv2[g], k);
+__device__ __forceinline__ void top_put(const Sim& S, MemSt& R, uint32_t i, const Key& k) {
+    const bool me = (uint32_t)S.lane == i;
+    R.g_tlo = me ? lo32(k.t) : R.g_tlo;
+    R.g_thi = me ? hi32(k.t) : R.g_thi;
+    R.g_s = me ? k.s : R.g_s;
+    R.g_c = me ? k.c : R.g_c;
 }
 __device__ __forceinline__ void top_load(const Sim& S, MemSt& R) {
-    if (!PRISMA_TOP_REG) return;
-    const uint32_t nt = PRISMA_LINK_TOP ? R.n_top : R.n2;
-    const uint4 k = ((uint32_t)S.lane < nt) ? R.lv2[S.lane] : make_uint4(0xffffffffu, 0x7fffffffu, 0xffffffffu, 0u);
+    const uint4 k = ((uint32_t)S.lane < R.n_top) ? R.topimg[S.lane] : make_uint4(0xffffffffu, 0x7fffffffu, 0xffffffffu, 0u);
     R.g_tlo = k.x; R.g_thi = k.y; R.g_s = k.z; R.g_c = k.w;
 }
 __device__ __forceinline__ void top_store(const Sim& S, const MemSt& R) {
-    if (!PRISMA_TOP_REG) return;
-    if ((uint32_t)S.lane < (PRISMA_LINK_TOP ? R.n_top : R.n2)) R.lv2[S.lane] = make_uint4(R.g_tlo, R.g_thi, R.g_s, R.g_c);
+    if ((uint32_t)S.lane < R.n_top) R.topimg[S.lane] = make_uint4(R.g_tlo, R.g_thi, R.g_s, R.g_c);
 }
 
-// ---- PRISMA_LINK_TOP tree: link blocks (LDS leaves) -> top; flow blocks (HBM leaves, LDS
-// level 1) -> flow groups -> top ----
+// ---- blocks and groups ----
+// minimum of link block b (64 link leaves, LDS)
 __device__ __forceinline__ Key lblock_min(const Sim& S, const MemSt& R, uint32_t b, int64_t now) {
     const uint32_t l = b * 64u + (uint32_t)S.lane;
     int64_t t = kInf;
@@ -238,6 +140,7 @@ __device__ __forceinline__ Key lblock_min(const Sim& S, const MemSt& R, uint32_t
     }
     return wave_min_key(t, s, (kind << 28) | l, now);
 }
+// minimum of flow block fb (64 flow leaves, HBM)
 __device__ __forceinline__ Key fblock_min(const Sim& S, const MemSt& R, uint32_t fb, int64_t now) {
     const uint32_t f = fb * 64u + (uint32_t)S.lane;
     int64_t t = kInf;
@@ -263,18 +166,23 @@ __device__ __forceinline__ Key fblock_min_cached(const Sim& S, const MemSt& R, u
     }
     return wave_min_key(t, s, (K_FLOW << 28) | fi, now);
 }
+// minimum of flow group g (64 flow block minima, LDS)
 __device__ __forceinline__ Key fgroup_min(const Sim& S, const MemSt& R, uint32_t g, int64_t now) {
     const uint32_t i = g * 64u + (uint32_t)S.lane;
     int64_t t = kInf;
     uint32_t s = 0xffffffffu, c = 0u;
     if (i < R.n_fb) {
-        const uint4 k = R.lv1[i];
+        const uint4 k = R.fblkmin[i];
         t = mk64(k.x, k.y);
         s = k.z;
         c = k.w;
     }
     return wave_min_key(t, s, c, now);
 }
+
+// Link l's next event changed to (t, seq) of kind `kind` (0: none): store its leaf and repair
+// its block's top lane.  The block is re-reduced only if the leaf was its minimum and did not
+// become smaller; a new smaller key simply replaces it.
 __device__ __forceinline__ void tree_touch_link(const Sim& S, MemSt& R, const Hot& H, uint32_t l, int64_t t,
                                                 uint32_t seq, uint32_t code, uint32_t kind) {
     R.lkey[l] = make_uint2(lo32(t), seq);                           // every lane: same address, same value
@@ -291,11 +199,13 @@ __device__ __forceinline__ void tree_touch_link(const Sim& S, MemSt& R, const Ho
     }
     top_put(S, R, b, nb);
 }
+// Flow (slot) f's next event changed to (t, seq) with draw index `draw`: its leaf, its block
+// minimum (LDS) and its group's top lane, each repaired only when it can change
 __device__ __forceinline__ void tree_touch_flow(const Sim& S, MemSt& R, const Hot& H, uint32_t f, int64_t t,
                                                 uint32_t seq, uint32_t draw) {
     st_rep(S, &R.fkeys[f], make_uint4(lo32(t), hi32(t), seq, draw));
     const uint32_t fb = f >> 6;
-    const Key cur = lds_key(&R.lv1[fb]);
+    const Key cur = lds_key(&R.fblkmin[fb]);
     Key nb;
     if (key_less(t, seq, cur.t, cur.s)) {
         nb.t = t; nb.s = seq; nb.c = (K_FLOW << 28) | f;
@@ -304,58 +214,18 @@ __device__ __forceinline__ void tree_touch_flow(const Sim& S, MemSt& R, const Ho
     } else {
         return;
     }
-    lds_put_key(S, &R.lv1[fb], nb);
-    const uint32_t g = fb >> 6, lane = R.n_lb + g;
-    const Key cg = top_key(R, lane);
+    lds_put_key(S, &R.fblkmin[fb], nb);
+    const uint32_t g = fb >> 6, i = R.n_lb + g;
+    const Key cg = top_key(R, i);
     Key ng;
     if (key_less(nb.t, nb.s, cg.t, cg.s)) {
         ng = nb;
-    } else if (((cg.c & 0x0fffffffu) >> 6) == fb) {
+    } else if (((cg.c & 0x0fffffffu) >> 6) == fb) {                // the group's minimum was this block's
         ng = fgroup_min(S, R, g, H.now);
     } else {
         return;
     }
-    top_put(S, R, lane, ng);
-}
-
-// Source `leaf`'s next event changed to (t, seq): store its key and repair the two
-// tree levels above it.  A block is re-reduced only if the leaf was its minimum and
-// did not become smaller; a new smaller key just replaces it.
-__device__ __forceinline__ void tree_touch(const Sim& S, MemSt& R, const Hot& H, uint32_t leaf, int64_t t,
-                                           uint32_t seq, uint32_t code, uint32_t aux) {
-    if (PRISMA_LINK_TOP) {
-        if (leaf < R.L) tree_touch_link(S, R, H, leaf, t, seq, code, aux);
-        else tree_touch_flow(S, R, H, leaf - R.L, t, seq, aux);
-        return;
-    }
-    if (leaf < R.L) {
-        R.lkey[leaf] = make_uint2(lo32(t), seq);              // every lane: same address, same value
-        R.lkind[leaf] = (uint8_t)aux;
-    } else {
-        st_rep(S, &R.fkeys[leaf - R.L], make_uint4(lo32(t), hi32(t), seq, aux));
-    }
-    const uint32_t b = leaf >> 6;
-    const Key cur = lds_key(&R.lv1[b]);
-    Key nb;
-    if (key_less(t, seq, cur.t, cur.s)) {
-        nb.t = t; nb.s = seq; nb.c = code;
-    } else if (leaf_of(R, cur.c) == leaf) {
-        nb = (b == R.fblk_b) ? block_min_cached(S, R, b, H.now, leaf, t, seq, code) : block_min(S, R, b, H.now);
-    } else {
-        return;
-    }
-    lds_put_key(S, &R.lv1[b], nb);
-    const uint32_t g = b >> 6;
-    const Key cg = top_key(R, g);
-    Key ng;
-    if (key_less(nb.t, nb.s, cg.t, cg.s)) {
-        ng = nb;
-    } else if (leaf_of(R, cg.c) == leaf_of(R, cur.c)) {
-        ng = group_min(S, R, g, H.now);
-    } else {
-        return;
-    }
-    top_put(S, R, g, ng);
+    top_put(S, R, i, ng);
 }
 
 // ---- links: the whole record is one coalesced load (lane j: word j) and the fields
@@ -404,26 +274,20 @@ __device__ __forceinline__ void link_put(const Sim& S, MemSt& R, const Hot& H, u
         if (kind == 0 || rw < rt || (rw == rt && k.wh_seq < s)) { t = k.wh_t; s = k.wh_seq; kind = K_ARRIVE; }
     }
     const int64_t at = kind ? H.now + (int64_t)(uint32_t)(t - n0) : kInf;
-    tree_touch(S, R, H, l, at, s, (kind << 28) | l, kind);
+    tree_touch_link(S, R, H, l, at, s, (kind << 28) | l, kind);
 }
 
 // ---- flows ----
 __device__ __forceinline__ void flow_min_refresh(const Sim&, MemSt&, const Hot&) {}   // the event tree keeps it
 __device__ __forceinline__ uint32_t flow_draw(const Sim& S, MemSt& R, uint32_t f) {
-    if (PRISMA_LINK_TOP) {                                          // flow blocks numbered from flow 0
-        const uint32_t fb = f >> 6, fi = fb * 64u + (uint32_t)S.lane;
-        R.fblk = fi < R.FG ? R.fkeys[fi] : make_uint4(0u, 0u, 0u, 0u);
-        R.fblk_b = fb;
-        return rdl(R.fblk.w, f & 63u);
-    }
-    const uint32_t leaf = R.L + f, b = leaf >> 6, li = b * 64u + (uint32_t)S.lane;
-    R.fblk = (li >= R.L && li < R.n_leaf) ? R.fkeys[li - R.L] : make_uint4(0u, 0u, 0u, 0u);
-    R.fblk_b = b;
-    return rdl(R.fblk.w, leaf & 63u);
+    const uint32_t fb = f >> 6, fi = fb * 64u + (uint32_t)S.lane;
+    R.fblk = fi < R.FG ? R.fkeys[fi] : make_uint4(0u, 0u, 0u, 0u);
+    R.fblk_b = fb;
+    return rdl(R.fblk.w, f & 63u);
 }
 __device__ __forceinline__ void flow_set(const Sim& S, MemSt& R, const Hot& H, uint32_t f, int64_t t, uint32_t seq,
                                          uint32_t draw) {
-    tree_touch(S, R, H, R.L + f, t, seq, (K_FLOW << 28) | f, draw);
+    tree_touch_flow(S, R, H, f, t, seq, draw);
     R.fblk_b = ~0u;
 }
 
@@ -498,45 +362,11 @@ __device__ __forceinline__ uint32_t observe_links(const Sim& S, const MemSt& R, 
     return p[LR_QB];
 }
 
-// observe_links in two halves (PRISMA_OBS_EARLY): the gather's loads, unconditional (lanes outside
-// 1..deg read link 0 and discard it), then the per-lane value
-__device__ __forceinline__ ObsG obs_issue(const Sim& S, const MemSt& R, uint32_t v) {
-    const int r0 = t_ovrow(S, v), deg = t_ovrow(S, v + 1) - r0;
-    const int lane = S.lane;
-    const uint32_t li = (lane >= 1 && lane <= deg) ? (uint32_t)(r0 + lane - 1) : 0u;
-    const uint32_t* p = R.lrec + li * R.RW;
-    ObsG g;
-    if (S.lv.ping_as_obs()) {
-        g.a = p[LR_PAVLO]; g.b = p[LR_PAVHI]; g.c = p[LR_PMLO]; g.d = p[LR_ODLO]; g.e = p[LR_ODHI];
-    } else {
-        g.a = p[LR_QB]; g.b = 0u; g.c = 0u; g.d = 0u; g.e = 0u;
-    }
-    return g;
-}
-__device__ __forceinline__ uint32_t obs_finish(const Sim& S, const MemSt&, const Hot& H, uint32_t v, const ObsG& g,
-                                               double now_s) {
-    const int deg = t_ovrow(S, v + 1) - t_ovrow(S, v);
-    const int lane = S.lane;
-    const uint32_t val = S.lv.ping_as_obs() ? ping_value_lane(ld_d(g.a, g.b), g.c, ld_d(g.d, g.e), H.ping_rounds, now_s)
-                                            : g.a;
-    return (lane >= 1 && lane <= deg) ? val : 0u;
-}
-
-// next event: minimum over the super-block minima and the ping timer
+// next event: minimum over the top level (VGPRs; infinite past n_top) and the ping timer
 __device__ __forceinline__ void select_event(const Sim& S, const MemSt& R, const Hot& H, int lane, int64_t& bt,
                                              uint32_t& bc, uint32_t& bs) {
-    int64_t t = kInf;
-    uint32_t s = 0xffffffffu, c = 0u;
-    if (PRISMA_TOP_REG) {
-        t = mk64(R.g_tlo, R.g_thi);                                 // (lanes >= n2: infinite)
-        s = R.g_s;
-        c = R.g_c;
-    } else if ((uint32_t)lane < R.n2) {
-        const uint4 k = R.lv2[lane];
-        t = mk64(k.x, k.y);
-        s = k.z;
-        c = k.w;
-    }
+    int64_t t = mk64(R.g_tlo, R.g_thi);
+    uint32_t s = R.g_s, c = R.g_c;
     if (lane == 0 && key_less(H.ping_t, H.ping_seq, t, s)) { t = H.ping_t; s = H.ping_seq; c = K_PING << 28; }
     const Key k = wave_min_key(t, s, c, H.now);
     bt = k.t;
@@ -579,21 +409,18 @@ __device__ __forceinline__ void mem_bind(Sim& S, MemSt& R, const KParams& P, con
     R.fkeys = (uint4*)(img + LC.g_keys);
     R.lkey = (uint2*)(lds + LC.s_lkey);
     R.lkind = (uint8_t*)(lds + LC.s_lkind);
-    R.lv1 = (uint4*)(lds + LC.s_lv1);
-    R.lv2 = (uint4*)(lds + LC.s_lv2);
+    R.fblkmin = (uint4*)(lds + LC.s_lv1);
+    R.topimg = (uint4*)(lds + LC.s_lv2);
     R.L = (uint32_t)LC.L;
-    R.n_leaf = LC.n_leaf;
-    R.n1 = LC.n1;
-    R.n2 = LC.n2;
+    R.FG = LC.n_leaf - R.L;
+    R.n_lb = (R.L + 63u) / 64u;                  // (layout_mem: n1 = n_fb flow blocks, n2 = n_top <= 64)
+    R.n_fb = LC.n1;
+    R.n_top = LC.n2;
     R.RW = LC.lrec_words;
     R.WCAP = (uint32_t)LC.WCAP;
     R.fblk = make_uint4(0u, 0u, 0u, 0u);
     R.fblk_b = ~0u;
     R.g_tlo = 0xffffffffu; R.g_thi = 0x7fffffffu; R.g_s = 0xffffffffu; R.g_c = 0u;
-    R.FG = R.n_leaf - R.L;
-    R.n_lb = (R.L + 63u) / 64u;
-    R.n_fb = (R.FG + 63u) / 64u;
-    R.n_top = R.n_lb + (R.n_fb + 63u) / 64u;
 }
 
 // episode start (sim.cc:610-630, data-packet-manager.cc:118-121): LDS header,
@@ -626,9 +453,7 @@ __device__ __forceinline__ void init_replica(Sim& S, MemSt& R, Hot& H, uint32_t 
     // apps in install order (fseq: with big signalling each generator right after its flow);
     // leaf F is the generators' slot (on_bsig), started at AppStartTime (sim.cc:244, 645)
     const uint32_t nbs = S.m_bs->n_gen;
-    for (uint32_t i = j; i < R.n_leaf; i += kWave) {
-        if (i < NL) continue;
-        const uint32_t f = i - NL;
+    for (uint32_t f = j; f < R.FG; f += kWave) {
         int64_t t = sec_to_ns(0.0001);
         if (f < (uint32_t)L.F()) {
             double U;
@@ -645,17 +470,11 @@ __device__ __forceinline__ void init_replica(Sim& S, MemSt& R, Hot& H, uint32_t 
         R.fkeys[f] = make_uint4(lo32(t), hi32(t), S.m_fseq[f], 0u);
     }
     __syncthreads();
-    if (PRISMA_LINK_TOP) {
-        for (uint32_t b = 0; b < R.n_lb; ++b) top_put(S, R, b, lblock_min(S, R, b, 0));
-        for (uint32_t fb = 0; fb < R.n_fb; ++fb) lds_put_key(S, &R.lv1[fb], fblock_min(S, R, fb, 0));
-        __syncthreads();
-        for (uint32_t g = 0; R.n_lb + g < R.n_top; ++g) top_put(S, R, R.n_lb + g, fgroup_min(S, R, g, 0));
-        top_store(S, R);
-    } else {
-        for (uint32_t b = 0; b < R.n1; ++b) lds_put_key(S, &R.lv1[b], block_min(S, R, b, 0));
-        __syncthreads();
-        for (uint32_t g = 0; g < R.n2; ++g) lds_put_key(S, &R.lv2[g], group_min(S, R, g, 0));
-    }
+    for (uint32_t b = 0; b < R.n_lb; ++b) top_put(S, R, b, lblock_min(S, R, b, 0));
+    for (uint32_t fb = 0; fb < R.n_fb; ++fb) lds_put_key(S, &R.fblkmin[fb], fblock_min(S, R, fb, 0));
+    __syncthreads();
+    for (uint32_t g = 0; R.n_lb + g < R.n_top; ++g) top_put(S, R, R.n_lb + g, fgroup_min(S, R, g, 0));
+    top_store(S, R);
     H.now = 0;
     H.ping_t = L.ping_period();
     H.ping_seq = 0;

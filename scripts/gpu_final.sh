@@ -3,6 +3,7 @@
 #   bash scripts/gpu_final.sh tests <tag>    smoke, the whole -m gpu suite, one bench line per BASELINE config
 #   bash scripts/gpu_final.sh prof1 <tag>    rocprofv3 kernel trace + PMC passes: headline, config 5
 #   bash scripts/gpu_final.sh prof2 <tag>    the same for configs 3 and 4
+#   bash scripts/gpu_final.sh rehearse <tag> the 8-GPU presets (config 4 sweep, config 5) as 2 ranks on cuda:0
 STAGE=$1
 TAG=${2:-x}
 P="python -u -m pytest -q --timeout 600 --timeout-method thread"
@@ -23,5 +24,11 @@ prof2)
   bash scripts/gpu_steps.sh \
     "timeout -k 10 550 bash scripts/profile_round.sh ${TAG}_aog --topology abilene_on_geant --policy dqn_buffer --cpu-baseline 0 > gpurun_out/prof_${TAG}_aog.log 2>&1; rc=\$?; tail -4 gpurun_out/prof_${TAG}_aog.log; exit \$rc" \
     "timeout -k 10 550 bash scripts/profile_round.sh ${TAG}_geant_mlp --topology geant --policy dqn_buffer --ping-as-obs 0 --replicas 2048 --cpu-baseline 0 > gpurun_out/prof_${TAG}_geant_mlp.log 2>&1; rc=\$?; tail -4 gpurun_out/prof_${TAG}_geant_mlp.log; exit \$rc"
+  ;;
+rehearse)
+  B="python bench.py --gpus 2 --same-device --steps 3 --warmup 1 --cpu-baseline 0"
+  bash scripts/gpu_steps.sh \
+    "timeout -k 10 400 $B --preset config4 --replicas 256 > gpurun_out/rehearse_${TAG}_config4.jsonl 2> gpurun_out/rehearse_${TAG}_config4.err; rc=\$?; cut -c1-200 gpurun_out/rehearse_${TAG}_config4.jsonl; exit \$rc" \
+    "timeout -k 10 400 $B --preset config5 --replicas 128 --warmup 2 > gpurun_out/rehearse_${TAG}_config5.jsonl 2> gpurun_out/rehearse_${TAG}_config5.err; rc=\$?; cut -c1-200 gpurun_out/rehearse_${TAG}_config5.jsonl; exit \$rc"
   ;;
 esac

@@ -19,10 +19,12 @@ if sys.argv[1] == "build":
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     sys.path.insert(0, ROOT)
     from prisma_amd import buildid
-    only = sys.argv[2:] and sys.argv[2] == "mem"
+    # `build mem` / `build lite_mlp`: that translation unit alone with the probes
+    only = {"mem": "prisma_engine_mem.hip", "lite_mlp": "prisma_engine_lite_mlp.hip",
+            "lite": "prisma_engine_lite.hip"}.get(sys.argv[2]) if sys.argv[2:] else None
     objs, procs = [], []
     for f in buildid.ENGINE_SOURCES:
-        if only and f != "prisma_engine_mem.hip":
+        if only and f != only:
             objs.append(os.path.join(ROOT, "prisma_amd", "csrc", os.path.splitext(f)[0] + ".o"))
             continue
         o = os.path.join(os.path.dirname(LIB), f + ".timing.o")

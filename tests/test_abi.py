@@ -168,9 +168,10 @@ def test_plan_engine_selection():
     m = engine.plan(ab, engine_params(ab, engine=engine.PRISMA_ENGINE_MEMORY))
     assert m["engine"] == engine.PRISMA_ENGINE_MEMORY and m["flow_slots"] == 0
     assert m["obs_width"] == 4 and m["record_bytes"] == 48
-    # 28 + 11 links and 110 flows: 149 leaves -> 3 level-1 nodes, 1 level-2 node, and the
-    # 39 link leaf keys (8 B) and kinds (1 B) in LDS, each region 16-B aligned
-    assert m["lds_state_bytes"] == 128 + 160 + 16 + 3 * 16 + 16 + 320 + 48
+    # 28 + 11 links and 110 flows: 2 flow blocks (LDS minima), a top level of 1 link block + 1
+    # flow group (its LDS image), and the 39 link leaf keys (8 B) and kinds (1 B), each region
+    # 16-B aligned
+    assert m["lds_state_bytes"] == 128 + 160 + 16 + 2 * 16 + 2 * 16 + 320 + 48
     n = 256
     ring = np.zeros((n, n), dtype=int)
     for i in range(n):
@@ -182,6 +183,19 @@ def test_plan_engine_selection():
     assert p["engine"] == engine.PRISMA_ENGINE_MEMORY
     with pytest.raises(engine.PrismaError, match="register-resident"):
         engine.plan(big, engine_params(big, engine=engine.PRISMA_ENGINE_REGISTER))
+    # the memory-resident event tree's top level is one VGPR per lane: link blocks + flow groups
+    # <= 64 (3 584 + 256 links = 60 link blocks: fits with one flow group, not with 16)
+    dense = np.zeros((n, n), dtype=int)
+    for i in range(n):
+        for d in range(1, 8):
+            dense[i, (i + d) % n] = dense[(i + d) % n, i] = 1
+    one = np.zeros((n, n), dtype=object)
+    one[0, 1] = 1000
+    assert engine.plan(Topology.from_matrices(dense, one), engine_params(Topology.from_matrices(dense, one)))[
+        "engine"] == engine.PRISMA_ENGINE_MEMORY
+    full = Topology.from_matrices(dense, tm)
+    with pytest.raises(engine.PrismaError, match="64 link blocks"):
+        engine.plan(full, engine_params(full))
     ov = Topology.example("overlay_full_mesh_3n_abilene")
     with pytest.raises(engine.PrismaError, match="identity overlays"):
         engine.plan(ov, engine_params(ov, engine=engine.PRISMA_ENGINE_MEMORY))
