@@ -1688,7 +1688,8 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
         }
     }
     TP0(6);
-    float h = det_elu(__fadd_rn(lane < 32 ? w1v : acc, b1v));
+    float h = (B == kMlpAll) ? det_elu_sel(__fadd_rn(lane < 32 ? w1v : acc, b1v))
+                             : det_elu(__fadd_rn(lane < 32 ? w1v : acc, b1v));
     if constexpr (kLnLds) __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
@@ -1700,16 +1701,16 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
         __builtin_amdgcn_wave_barrier();
         return lane_argmin_first_seq(q4, deg);
     }
-    if constexpr (PRE && PRISMA_PRE_W2) h = det_elu(mlp_dense64_pre(S, P1.w2, P1.b2));
-    else if constexpr (PRE) h = det_elu(mlp_dense64_pre(S, M.w2, M.b2));
-    else if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w2, M.b2));
+    if constexpr (PRE && PRISMA_PRE_W2) h = det_elu_sel(mlp_dense64_pre(S, P1.w2, P1.b2));
+    else if constexpr (PRE) h = det_elu_sel(mlp_dense64_pre(S, M.w2, M.b2));
+    else if constexpr (B == kMlpAll) h = det_elu_sel(mlp_dense64_pre(S, M.w2, M.b2));
     else h = det_elu(mlp_dense64<B>(S, RP, lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
     __builtin_amdgcn_wave_barrier();
     TP0(8);
     TM_MLP(1);
-    if constexpr (B == kMlpAll) h = det_elu(mlp_dense64_pre(S, M.w3, M.b3));
+    if constexpr (B == kMlpAll) h = det_elu_sel(mlp_dense64_pre(S, M.w3, M.b3));
     else h = det_elu(mlp_dense64<B>(S, RP + mlp_rp_layer_floats(64), lane, 64));
     __builtin_amdgcn_wave_barrier();
     S.hbuf[lane] = h;
@@ -1718,7 +1719,7 @@ __device__ __forceinline__ int mlp_action(const Sim& S, uint32_t v, uint32_t obs
     TM_MLP(2);
     float q = 0.0f;
     if constexpr (B == kMlpAll) {
-        const float q4 = det_elu(mlp_dense64_pre(S, M.w4, M.b4));
+        const float q4 = det_elu_sel(mlp_dense64_pre(S, M.w4, M.b4));
         if (lane < deg) q = q4;
     } else {
         if (lane < deg) q = det_elu(mlp_dense64<B>(S, RP + 2 * mlp_rp_layer_floats(64), lane, D));

@@ -106,15 +106,15 @@ __host__ __device__ inline float det_expm1f(float x) {
 }
 
 // Keras ELU (alpha 1): x > 0 ? x : expm1(x)
-// PRISMA_ELU_SELECT (device): every lane computes the expm1 branch and the result is selected --
-// the branches had been exec-mask regions around ~25 instructions (round 5: config 5 +1.7 %)
-#ifndef PRISMA_ELU_SELECT
-#define PRISMA_ELU_SELECT 1
-#endif
-__host__ __device__ inline float det_elu(float x) {
-#if defined(__HIP_DEVICE_COMPILE__) && PRISMA_ELU_SELECT
-    // det_expm1f's operations on every lane and its cases as selects (no exec-mask branches);
-    // the selected value is the same operation sequence's, so the bits equal det_elu's
+__host__ __device__ inline float det_elu(float x) { return x > 0.0f ? x : det_expm1f(x); }
+
+// det_elu without branches (the memory-resident engine's MLP, one wave per SIMD): det_expm1f's
+// operations on every lane and its cases as selects -- the selected value is the same operation
+// sequence's, so the bits equal det_elu's.  The branches had been exec-mask regions around ~25
+// instructions (round 5: config 5 +1.7 %); the register-resident instances keep det_elu (at 2-4
+// waves per SIMD the extra lanes' work and registers cost them 35-60 %).
+__host__ __device__ inline float det_elu_sel(float x) {
+#ifdef __HIP_DEVICE_COMPILE__
     const float t = x * 1.44269504f + 0.5f;
     int ki = (int)t;
     ki = ((float)ki > t) ? ki - 1 : ki;
@@ -132,7 +132,7 @@ __host__ __device__ inline float det_elu(float x) {
     const float m = (x < -17.0f) ? -1.0f : ((x > -5.9604645e-08f) ? x : e);
     return (x > 0.0f || !(x == x)) ? x : m;
 #else
-    return x > 0.0f ? x : det_expm1f(x);
+    return det_elu(x);
 #endif
 }
 
