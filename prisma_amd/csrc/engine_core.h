@@ -741,8 +741,10 @@ __device__ __forceinline__ bool ring_store_needed(const Sim& S, const LinkV& k) 
 template <class RS>
 __device__ __forceinline__ int link_send_k(const Sim& S, RS& R, Hot& H, uint32_t l, uint32_t e, LinkV k) {
     const LV& L = S.lv;
+    TP1_START();
     uint32_t size = ent_size(S, e, l);
     bool ok = l < (uint32_t)L.E() ? (k.qb + size <= L.qmax_bytes()) : (k.n_queue + 1u <= L.acc_qmax_pkts());
+    TP1(11);
     if (!ok) return 0;
     if (RS::kLazy) {
         // the transmitter's completion was elided (nothing queued behind it): if it precedes
@@ -757,6 +759,7 @@ __device__ __forceinline__ int link_send_k(const Sim& S, RS& R, Hot& H, uint32_t
     k.tail = (k.tail + 1 == cap) ? 0 : k.tail + 1;
     k.n_queue++;
     k.qb += size;
+    TP1(12);
     if (!k.busy) {                                              // :643-650
         uint32_t xi = k.txp;
         uint32_t hx = (k.n_queue == 1) ? e : u_ld32(&S.ring[off + xi]);
@@ -766,7 +769,9 @@ __device__ __forceinline__ int link_send_k(const Sim& S, RS& R, Hot& H, uint32_t
         k.qb -= ent_size(S, hx, l);
         transmit_start(S, H, l, k, xi, hx);
     }
+    TP1(13);
     link_put(S, R, H, l, k);
+    TP1(15);
     return 1;
 }
 template <class RS>
@@ -1808,10 +1813,22 @@ __device__ __forceinline__ void ping_ack(const Sim& S, RS& R, Hot& H, uint32_t l
     // refresh the cached window mean (data-packet-manager.cc:55-65), summed oldest first
     double sum = 0.0;
     uint32_t i = wh;
-    for (uint32_t j = 0; j < wn; ++j) {
-        float w = (i == slot) ? delay : __uint_as_float(u_ld32((const uint32_t*)S.win + lt * MA + i));
-        sum += (double)w;
-        i = (i + 1 == MA) ? 0 : i + 1;
+    if constexpr (RS::kMem) {
+        // the memory-resident engine's windows are in HBM: one load of the whole window (lane m:
+        // slot m), then the slots in order through readlanes -- one round trip instead of one per
+        // slot (the loop had waited for each load in turn; round 5, config 5 +0.2 %)
+        const uint32_t wl = ((uint32_t)S.lane < MA) ? ((const uint32_t*)S.win)[lt * MA + (uint32_t)S.lane] : 0u;
+        for (uint32_t j = 0; j < wn; ++j) {
+            const float w = (i == slot) ? delay : __uint_as_float(rdl(wl, i));
+            sum += (double)w;
+            i = (i + 1 == MA) ? 0 : i + 1;
+        }
+    } else {
+        for (uint32_t j = 0; j < wn; ++j) {
+            float w = (i == slot) ? delay : __uint_as_float(u_ld32((const uint32_t*)S.win + lt * MA + i));
+            sum += (double)w;
+            i = (i + 1 == MA) ? 0 : i + 1;
+        }
     }
     ping_set_win(S, R, lt, pw_new, (uint64_t)__double_as_longlong(sum / (double)wn));
 }

@@ -99,7 +99,7 @@ if buf[20]:
 # fine probes TP(i) (engine_core.h): cycles since the previous probe, per execution
 PROBES = (["arr:record", "arr:issue-prev+obs", "arr:wire-pop+tree", "arr:prev-wait", "arr:data-rest",
            "arr:ctl-pop", "arr:ctl-rest", "cmp:record", "cmp:ring", "cmp:transmit", "cmp:put+tree",
-           "p11", "p12", "p13", "p14", "p15"] if os.environ.get("PRISMA_TP_SET") == "1" else
+           "flowsend:admit", "flowsend:ring", "flowsend:transmit", "put:store", "put:tree"] if os.environ.get("PRISMA_TP_SET") == "1" else
           ["mlp:wait-arrival", "mlp:sum", "mlp:w3-issue", "mlp:var", "mlp:w4-issue", "mlp:den+xn",
           "mlp:l1-chunks", "mlp:l1-elu+store", "mlp:l2", "mlp:l3", "mlp:l4", "mlp:argmin",
           "dec:send", "dec:record+cnt", "probe14", "probe15"])
