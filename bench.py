@@ -46,12 +46,15 @@ HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 # BASELINE.json configs, per GPU (weak scaling): explicit flags override these values
 PRESETS = {
     "config1": dict(topology="abilene", policy="sp", replicas=1, ping_as_obs=1, hops=2048),
-    "config2": dict(topology="abilene", policy="dq_routing", replicas=4096, ping_as_obs=1),
-    "config3": dict(topology="abilene_on_geant", policy="dqn_buffer", replicas=4096, ping_as_obs=1),
-    "config4": dict(topology="geant", policy="dqn_buffer", replicas=2048, ping_as_obs=0,
+    "config2": dict(topology="abilene", policy="dq_routing", replicas=4096, ping_as_obs=1, hops=32768),
+    "config3": dict(topology="abilene_on_geant", policy="dqn_buffer", replicas=4096, ping_as_obs=1, hops=8192),
+    "config4": dict(topology="geant", policy="dqn_buffer", replicas=2048, ping_as_obs=0, hops=8192,
                     load_factors="0.5,0.75,1.0,1.25,1.5,1.75,2.0"),
-    "config5": dict(topology="er256", policy="dqn_buffer", replicas=1024, ping_as_obs=1),
+    "config5": dict(topology="er256", policy="dqn_buffer", replicas=1024, ping_as_obs=1, hops=8192),
 }
+# hops per replica per step: 32 768 for the headline (config2, also a run with no workload flags:
+# one launch of ~0.16 s, the per-step policy refresh and launch costs amortised, and a default run
+# keeps the GPU busy for seconds, not the ~1 s of round 4 against ~17 s of CPU baseline); 8 192 else
 DEFAULTS = dict(topology="abilene", policy="dq_routing", ping_as_obs=1, hops=8192, load_factor=1.0)
 
 
@@ -68,8 +71,9 @@ def parse(argv=None):
                         "flow-start events are a transient of the episode)")
     p.add_argument("--replicas", type=int, default=None, help="replicas per GPU (default 4096; er256: 1024 = "
                                                              "BASELINE config 5's 8192 over 8 GPUs)")
-    p.add_argument("--hops", type=int, default=None, help="hops per replica per step (default 8192: one launch "
-                   "of ~60 ms at the headline, so the per-step policy refresh and launch costs stay ~1 %%)")
+    p.add_argument("--hops", type=int, default=None, help="hops per replica per step (default 32768 at the "
+                   "headline: one launch of ~0.16 s, so the per-step policy refresh and launch costs stay well "
+                   "under 1 %%; 8192 in the config3-5 presets)")
     p.add_argument("--topology", default=None)
     p.add_argument("--tm", type=int, default=0)
     p.add_argument("--load-factor", type=float, default=None)
@@ -97,6 +101,8 @@ def parse(argv=None):
     p.add_argument("--backend", default=None, choices=["nccl", "gloo"],
                    help="process-group backend (default: nccl = RCCL; gloo with --same-device)")
     a = p.parse_args(argv)
+    if a.preset is None and a.topology is None and a.policy is None and a.replicas is None:
+        a.preset = "config2"                     # the driver's default run: the headline
     for k, v in (PRESETS[a.preset] if a.preset else {}).items():
         if getattr(a, k) is None:
             setattr(a, k, v)
