@@ -14,9 +14,9 @@ echo "config 3: abilene on geant, DQN-buffer pingAsObs=1, 4096" && $B --preset c
 echo "config 3 (SP table)" && $B --preset config3 --policy sp --cpu-baseline 0 >> $OUT
 echo "config 4: geant DQN-buffer pingAsObs=0, 2048, lf 0.5 ... 2.0" && $B --preset config4 --cpu-baseline $C >> $OUT
 echo "config 4 variant: geant DQN-buffer pingAsObs=1 lf 1.0, 2048" && $B --preset config4 --ping-as-obs 1 --load-factors 1.0 --cpu-baseline 0 >> $OUT
-# ER-256: 13 warmup steps (8 192 hops each) past the first simulated second's flow-start transient
-echo "config 5: ER-256 DQN-buffer pingAsObs=1, 1024" && $B --preset config5 --warmup 13 --cpu-baseline $C >> $OUT
-echo "config 5 (SP table)" && $B --preset config5 --policy sp --warmup 13 --cpu-baseline 0 >> $OUT
+# ER-256: the preset's 4 warmup steps (32 768 hops each) pass the first simulated second's flow-start transient
+echo "config 5: ER-256 DQN-buffer pingAsObs=1, 1024" && $B --preset config5 --warmup 4 --cpu-baseline $C >> $OUT
+echo "config 5 (SP table)" && $B --preset config5 --policy sp --warmup 4 --cpu-baseline 0 >> $OUT
 python - <<'PY'
 import json
 for l in open("gpurun_out/configs.jsonl"):

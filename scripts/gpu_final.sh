@@ -18,12 +18,12 @@ tests)
 prof1)
   bash scripts/gpu_steps.sh \
     "timeout -k 10 550 bash scripts/profile_round.sh ${TAG} > gpurun_out/prof_${TAG}.log 2>&1; rc=\$?; tail -4 gpurun_out/prof_${TAG}.log; exit \$rc" \
-    "timeout -k 10 550 bash scripts/profile_round.sh ${TAG}_er256 --topology er256 --policy dqn_buffer --warmup 13 --cpu-baseline 0 > gpurun_out/prof_${TAG}_er256.log 2>&1; rc=\$?; tail -4 gpurun_out/prof_${TAG}_er256.log; exit \$rc"
+    "timeout -k 10 550 bash scripts/profile_round.sh ${TAG}_er256 --preset config5 --warmup 4 --cpu-baseline 0 > gpurun_out/prof_${TAG}_er256.log 2>&1; rc=\$?; tail -4 gpurun_out/prof_${TAG}_er256.log; exit \$rc"
   ;;
 prof2)
   bash scripts/gpu_steps.sh \
-    "timeout -k 10 550 bash scripts/profile_round.sh ${TAG}_aog --topology abilene_on_geant --policy dqn_buffer --cpu-baseline 0 > gpurun_out/prof_${TAG}_aog.log 2>&1; rc=\$?; tail -4 gpurun_out/prof_${TAG}_aog.log; exit \$rc" \
-    "timeout -k 10 550 bash scripts/profile_round.sh ${TAG}_geant_mlp --topology geant --policy dqn_buffer --ping-as-obs 0 --replicas 2048 --cpu-baseline 0 > gpurun_out/prof_${TAG}_geant_mlp.log 2>&1; rc=\$?; tail -4 gpurun_out/prof_${TAG}_geant_mlp.log; exit \$rc"
+    "timeout -k 10 550 bash scripts/profile_round.sh ${TAG}_aog --preset config3 --cpu-baseline 0 > gpurun_out/prof_${TAG}_aog.log 2>&1; rc=\$?; tail -4 gpurun_out/prof_${TAG}_aog.log; exit \$rc" \
+    "timeout -k 10 550 bash scripts/profile_round.sh ${TAG}_geant_mlp --preset config4 --load-factors 1.0 --cpu-baseline 0 > gpurun_out/prof_${TAG}_geant_mlp.log 2>&1; rc=\$?; tail -4 gpurun_out/prof_${TAG}_geant_mlp.log; exit \$rc"
   ;;
 rehearse)
   B="python bench.py --gpus 2 --same-device --steps 3 --warmup 1 --cpu-baseline 0"

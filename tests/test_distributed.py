@@ -126,4 +126,4 @@ def test_bench_presets_rendezvous_gloo_world2(preset):
         assert d["replicas_gathered"] == 4096
     else:
         assert w["topology"] == "er256" and w["ping_as_obs"] == 1 and w["replicas_per_gpu"] == 1024
-        assert w["load_factors"] == [1.0] and d["replicas_gathered"] == 2048 and w["warmup"] == 13
+        assert w["load_factors"] == [1.0] and d["replicas_gathered"] == 2048 and w["warmup"] == 4
