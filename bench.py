@@ -47,17 +47,17 @@ HBM_PEAK_GBS = 8000.0                    # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 PRESETS = {
     "config1": dict(topology="abilene", policy="sp", replicas=1, ping_as_obs=1, hops=2048),
     "config2": dict(topology="abilene", policy="dq_routing", replicas=4096, ping_as_obs=1, hops=32768),
-    "config3": dict(topology="abilene_on_geant", policy="dqn_buffer", replicas=4096, ping_as_obs=1, hops=32768),
-    "config4": dict(topology="geant", policy="dqn_buffer", replicas=2048, ping_as_obs=0, hops=32768,
+    "config3": dict(topology="abilene_on_geant", policy="dqn_buffer", replicas=4096, ping_as_obs=1, hops=8192),
+    "config4": dict(topology="geant", policy="dqn_buffer", replicas=2048, ping_as_obs=0, hops=8192,
                     load_factors="0.5,0.75,1.0,1.25,1.5,1.75,2.0"),
     # (4 warm-up steps x 32 768 hops: past the first simulated second's 65 251 flow starts)
     "config5": dict(topology="er256", policy="dqn_buffer", replicas=1024, ping_as_obs=1, hops=32768, warmup=4),
 }
-# hops per replica per step in the BASELINE presets: 32 768 (config2 -- also a run with no workload
-# flags -- to config5): one launch of 0.16 - 0.45 s, so the per-step policy refresh, the launch and the
-# launch's tail (the last replica to finish its hops ends it; at one wave per SIMD, config 5 gains 4 %
-# from 8 192 to 32 768 hops) are amortised, and a default run keeps the GPU busy for seconds, not the
-# ~1 s of round 4 against ~17 s of CPU baseline; 8 192 for ad-hoc workloads
+# hops per replica per step in the BASELINE presets, each the better of 8 192 and 32 768 measured on
+# build efc0e356bcf3: 32 768 for config2 (also a run with no workload flags: +0.9 %, and a default run
+# keeps the GPU busy for seconds, not the ~1 s of round 4 against ~17 s of CPU baseline) and config5
+# (+3.8 %: the launch's tail -- the last replica to finish its hops ends it, at one wave per SIMD --
+# amortised); 8 192 for config3 and config4 (-2.5 % / -1 % at 32 768) and ad-hoc workloads
 DEFAULTS = dict(topology="abilene", policy="dq_routing", ping_as_obs=1, hops=8192, load_factor=1.0)
 
 

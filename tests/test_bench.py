@@ -17,7 +17,7 @@ from prisma_amd.topology import Topology, sp_next_hop_table  # noqa: E402
 def test_presets_and_overrides():
     a = bench.parse(["--preset", "config4"])
     assert (a.topology, a.policy, a.replicas, a.ping_as_obs) == ("geant", "dqn_buffer", 2048, 0)
-    assert a.lfs == [0.5, 0.75, 1.0, 1.25, 1.5, 1.75, 2.0] and a.hops == 32768
+    assert a.lfs == [0.5, 0.75, 1.0, 1.25, 1.5, 1.75, 2.0] and a.hops == 8192
     assert bench.parse(["--preset", "config5"]).hops == 32768 and bench.parse(["--preset", "config2"]).hops == 32768
     a = bench.parse(["--preset", "config4", "--load-factors", "1.0,2.0", "--replicas", "64", "--ping-as-obs", "1"])
     assert a.lfs == [1.0, 2.0] and a.replicas == 64 and a.ping_as_obs == 1
