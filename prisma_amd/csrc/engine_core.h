@@ -66,18 +66,28 @@ static __device__ unsigned long long g_prisma_timing[kTimingWords];
 #define TP(i) do { } while (0)
 #endif
 // probe sets (timing build, -DPRISMA_TP_SET): 0 the decision (mlp_action, apply_decision), 1 the
-// memory-resident arrival / completion / flow handlers
+// memory-resident arrival / completion / flow handlers, 2 the register-resident ones
 #ifndef PRISMA_TP_SET
 #define PRISMA_TP_SET 0
 #endif
 #if PRISMA_TP_SET == 0
 #define TP0(i) TP(i)
-#define TP1(i) do { } while (0)
-#define TP1_START() do { } while (0)
 #else
 #define TP0(i) do { } while (0)
+#endif
+#if PRISMA_TP_SET == 1
 #define TP1(i) TP(i)
 #define TP1_START() TP_START()
+#else
+#define TP1(i) do { } while (0)
+#define TP1_START() do { } while (0)
+#endif
+#if PRISMA_TP_SET == 2
+#define TP2(i) do { if (!S.mem) TP(i); } while (0)
+#define TP2_START() do { if (!S.mem) TP_START(); } while (0)
+#else
+#define TP2(i) do { } while (0)
+#define TP2_START() do { } while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -819,9 +829,11 @@ template <class RS>
 __device__ __forceinline__ void on_complete(const Sim& S, RS& R, Hot& H, uint32_t l) {   // :305-336
     const LV& L = S.lv;
     if (S.mem) TP1_START();
+    TP2_START();
     LinkV k = link_get(R, l);
     k.busy = 0;
     if (S.mem) TP1(7);
+    TP2(11);
     if (k.n_queue) {
         uint32_t cap = ring_cap(S, l);
         uint32_t xi = k.txp;
@@ -834,8 +846,10 @@ __device__ __forceinline__ void on_complete(const Sim& S, RS& R, Hot& H, uint32_
         transmit_start(S, H, l, k, xi, hx);
     }
     if (S.mem) TP1(9);
+    TP2(12);
     link_put(S, R, H, l, k);
     if (S.mem) TP1(10);
+    TP2(13);
 }
 
 // ---- observation (data-packet-manager.cc:171-206)
@@ -991,6 +1005,37 @@ __device__ __forceinline__ uint32_t tunnel_link(const Sim& S, uint32_t t) {
     return S.tun ? ti_link(S.T->tinfo[t]) : t;
 }
 
+// Relay entries carry (decision, live TTL, tunnel target) -- rip_make, engine_layout.h -- in the
+// register-resident engine's tunnelled-overlay kernels without the --train / notify_dest paths
+// (a compile-time constant): a switch inside a tunnel forwards a data packet on its entry alone,
+// as IpForward does on the IP header (ipv4-l3-protocol.cc IpForward), instead of reading the
+// deciding node, action and TTL back from the decision record in HBM.
+__device__ __forceinline__ bool relay_ip(const Sim& S) { return S.tun && !S.mem && !S.ctrl; }
+__device__ __forceinline__ uint32_t relay_dist(const Sim& S, uint32_t d, uint32_t x) {
+    return relay_ip(S) ? (d - rip_dec(x)) & kRipMask : (d - r_dec(x)) & kRelayMask;
+}
+// byte offsets of record words 6 (node | dst << 8 | start << 16) and 7 (action | status << 8 |
+// TTL << 16 | episode << 24): write_record
+__device__ __forceinline__ uint32_t record_word(const Sim& S, uint32_t d, uint32_t off) {
+    return rfl(*(const uint32_t*)(S.logrep + (size_t)(d & (S.lv.log_cap() - 1)) * S.lv.rec_bytes() + off));
+}
+// a relayed data packet dropped on an intermediate FIFO: point-to-point-net-device.cc:655-664 at
+// switch v, MacTxDrop -> the sender's loss (data-packet-manager.cc:88-98, forwarder.py:214-244)
+__device__ __forceinline__ void relay_dropped(const Sim& S, uint32_t dd, uint32_t dst, uint32_t v) {
+    const LV& L = S.lv;
+    if (dst != v) {
+        CNT_ADD(S, ov_lost, 1u);
+        CNT_ADD(S, cost_sum, L.loss_penalty_f());
+        CNT_ADD(S, cost_n, 1u);
+    } else {
+        CNT_ADD(S, un_lost, 1u);
+        CNT_ADD(S, un_cost_sum, L.loss_penalty_f());
+        CNT_ADD(S, un_cost_n, 1u);
+    }
+    patch_status(S, dd, PRISMA_ST_DROPPED);
+    CNT_ADD(S, reward_sum, L.loss_penalty());
+}
+
 // DataPacketManager::sendPacket (data-packet-manager.cc:251-299) for decision
 // d at node v, then the Receive tail.  x is the arriving entry (for the
 // counters); fused: the record is written here once, with the final status
@@ -1006,17 +1051,21 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
 #endif
     // ExecuteActions (packet-routing-gym.cc:203-208): the --train echo goes first
     if (echo_link != kNoLink) send_echo(S, R, H, echo_link, uid, last);
+    TP2_START();
     v = rfl(v);                                     // (scalar loads of the row pointers)
     int r0 = t_ovrow(S, v), deg = t_ovrow(S, v + 1) - r0;
     uint32_t status;
     if ((uint32_t)action < (uint32_t)deg) {                      // 0 <= action < deg
-        const uint32_t l = tunnel_link(S, (uint32_t)(r0 + action));   // RouteOutput (:281-287)
+        const uint32_t tiw = S.tun ? (uint32_t)S.T->tinfo[(uint32_t)(r0 + action)] : 0u;
+        const uint32_t l = S.tun ? ti_link(tiw) : (uint32_t)(r0 + action);   // RouteOutput (:281-287)
         CNT_ADD(S, hops, 1u);
         CNT_ADD(S, hop_deg_sum, (uint64_t)deg);
         // (memory-resident engine without the ctrl paths: the destination instead of the
         // source, engine_layout.h)
         const uint32_t src = (RS::kMem && !S.ctrl) ? dst : ent_src(x, v);
-        const uint32_t fwd = (PRISMA_ABLATE & 1) ? (T_RELAY | (dst << 2) | (start << 10) | (src << 24)) : r_make(d, src);
+        const uint32_t fwd = relay_ip(S) ? rip_make(d, ttl, ti_tgt(tiw))
+                           : ((PRISMA_ABLATE & 1) ? (T_RELAY | (dst << 2) | (start << 10) | (src << 24)) : r_make(d, src));
+        TP2(7);
         if (link_send(S, R, H, l, fwd)) {                         // lastHop = v, previous decision = d
             status = PRISMA_ST_ENQUEUED;
         } else {
@@ -1033,9 +1082,12 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
     { const uint64_t t = TM_NOW(); S.tsub[0] += t - S.tlast; S.tlast = t; }
 #endif
     TP0(12);
+    TP2(8);
     if (fused) write_record(S, H, d, reward, uid, prev, v, dst, start, action, status, obs_reg, ttl);
     else patch_record(S, H, d, action, status);
+    TP2(9);
     receive_counters(S, R, H, x, false, 0u, 0u);
+    TP2(10);
 #if PRISMA_TIMING
     { const uint64_t t = TM_NOW(); S.tsub[1] += t - S.tlast; S.tlast = t; }
 #endif
@@ -1062,8 +1114,11 @@ __device__ __forceinline__ int finish_pending(const Sim& S, RS& R, Hot& H, int a
         receive_counters(S, R, H, x, true, u_ld32(&h.pend_ent[2]), 0u);
         return 0;
     }
-    apply_decision(S, R, H, x, 0u, 0u, u_ld32(&h.pend_uid), u_ld32(&h.pend_node), u_ld32(&h.pend_dec), action,
-                   false, 0.0, 0, 0u, echo_link, last, 0u);
+    // (relay entries with the TTL: the pending decision's, from its record)
+    const uint32_t pdec = u_ld32(&h.pend_dec);
+    const uint32_t ttl = relay_ip(S) ? (record_word(S, pdec, 28) >> 16) & 255u : 0u;
+    apply_decision(S, R, H, x, 0u, 0u, u_ld32(&h.pend_uid), u_ld32(&h.pend_node), pdec, action,
+                   false, 0.0, 0, 0u, echo_link, last, ttl);
     return 1;
 }
 
@@ -1204,13 +1259,16 @@ __device__ __forceinline__ void on_flow(const Sim& S, RS& R, Hot& H, uint32_t f)
         TM_FLOW(1);
     } else {
         if (S.ctrl && f >= (uint32_t)S.lv.F()) { on_bsig(S, R, H, f); return; }
+        TP2_START();
         draw = flow_draw(S, R, f);
         if (draw != 0) {
             const uint32_t src = (uint32_t)t_fsrc(S, f);
             const uint32_t par = (uint32_t)(TSEC(H.now)) & 1u;
+            TP2(14);
             link_send(S, R, H, (uint32_t)S.lv.E() + src, f_make((uint32_t)t_fdst(S, f), par, H.uid & kUidMask));
             H.uid++;
         }
+        TP2(15);
     }
     flow_next(S, R, H, f, draw);                                    // StartSending / ScheduleNextTx
 }
@@ -1846,6 +1904,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
                                          MlpPre1& Mpre) {
     const LV& L = S.lv;
     if (S.mem) TP1_START();
+    TP2_START();
     const uint32_t v = (uint32_t)t_ldst(S, l);
     LinkV k = link_get(R, l);
     const uint32_t wh = k.head & (uint32_t)(L.WCAP() - 1);
@@ -1853,8 +1912,23 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
                              : (S.tun ? u_ld32(&S.went[l * (uint32_t)L.WCAP() + wh])
                                       : u_ld32(&S.ring[ring_off(S, l) + k.head]));
     if (S.mem) TP1(0);
+    TP2(0);
     const uint32_t type = ent_type(x);
     const bool tun = S.tun;
+    if (relay_ip(S) && type == T_RELAY && rip_tgt(x) != v) {
+        // a switch inside the packet's tunnel: IP-forwarded towards the tunnel's target
+        // (packet-manager.cc:115 -> not valid, no Notify) on the entry alone
+        wire_pop(S, R, H, l, k);
+        const uint32_t d = H.dec, dist = relay_dist(S, d, x);
+        if (dist >= L.log_cap()) fail(H, PRISMA_EBIT_LOGWRAP);
+        // IpForward decrements the TTL first and drops at 0 (no trace, no counter)
+        const uint32_t tt = rip_ttl(x);
+        if (tt == 1u) return 0;
+        const uint32_t xf = tt == kRipTtlSat ? x : x - (1u << 20);
+        if (!link_send(S, R, H, ti_link(route(S, v, rip_tgt(x))), xf))
+            relay_dropped(S, d - dist, (record_word(S, d - dist, 24) >> 8) & 255u, v);
+        return 0;
+    }
     if (ent_is_data(x)) {
         // PacketRoutingEnv::NotifyPktRcv -> Notify (packet-routing-gym.cc:231-267)
         // A forwarded packet's previous decision record (t_ns, uid, dst,
@@ -1866,7 +1940,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         // (A fresh packet loads and ignores some record of its own log: the
         // load and its consumption are unconditional on this path.)
         const uint32_t d = H.dec;
-        const uint32_t dist = (d - r_dec(x)) & kRelayMask;
+        const uint32_t dist = relay_dist(S, d, x);
         const unsigned char* pr = S.logrep + (size_t)((d - dist) & (L.log_cap() - 1)) * L.rec_bytes();
         const uint4 ph = *(const uint4*)pr;
         const uint2 pw = *(const uint2*)(pr + 24);
@@ -1885,8 +1959,10 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         // nothing touches before the decision)
         const uint32_t obs_early = S.mem ? observe_links(S, R, H, v, ns_to_sec(H.now)) : 0u;
         if (S.mem) TP1(1);
+        TP2(1);
         wire_pop(S, R, H, l, k);
         if (S.mem) TP1(2);
+        TP2(2);
         uint32_t ttl = 255u;                                        // SetIpTtl(255) (poisson-application.cc:330)
         if (tun && type == T_RELAY) {
             // Tunnelled overlay: the packet's next hop is the target of the tunnel
@@ -1897,25 +1973,14 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
             const uint32_t ti = S.T->tinfo[(uint32_t)t_ovrow(S, u) + (w7p & 255u)];
             const uint32_t ttl_prev = (w7p >> 16) & 255u;
             if (ti_tgt(ti) != v) {
+                // (relay_ip: the entry named this node as the target, so the record is not this
+                // packet's -- the log wrapped past the 18-bit decision index)
+                if (relay_ip(S)) { fail(H, PRISMA_EBIT_LOGWRAP); return 0; }
                 if (dist >= L.log_cap()) fail(H, PRISMA_EBIT_LOGWRAP);
                 // IpForward decrements the TTL first and drops at 0 (no trace, no counter)
                 if (ttl_prev == (route(S, u, v) >> 8)) return 0;
-                if (!link_send(S, R, H, ti_link(route(S, v, ti_tgt(ti))), x)) {
-                    // dropped on an intermediate FIFO: point-to-point-net-device.cc:655-664 at this
-                    // node, MacTxDrop -> the sender's loss (data-packet-manager.cc:88-98,
-                    // forwarder.py:214-244)
-                    if (((w6p >> 8) & 255u) != v) {
-                        CNT_ADD(S, ov_lost, 1u);
-                        CNT_ADD(S, cost_sum, L.loss_penalty_f());
-                        CNT_ADD(S, cost_n, 1u);
-                    } else {
-                        CNT_ADD(S, un_lost, 1u);
-                        CNT_ADD(S, un_cost_sum, L.loss_penalty_f());
-                        CNT_ADD(S, un_cost_n, 1u);
-                    }
-                    patch_status(S, d - dist, PRISMA_ST_DROPPED);
-                    CNT_ADD(S, reward_sum, L.loss_penalty());
-                }
+                if (!link_send(S, R, H, ti_link(route(S, v, ti_tgt(ti))), x))
+                    relay_dropped(S, d - dist, (w6p >> 8) & 255u, v);
                 return 0;
             }
             ttl = ttl_prev - (ti_len(ti) - 1u);
@@ -1925,6 +1990,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         const int64_t t_prev = mk64(rfl(ph.x), rfl(ph.y));
         const uint32_t uid_prev = rfl(ph.z), w_prev = rfl(pw.x);
         if (S.mem) TP1(3);
+        TP2(3);
         double reward = 0.0;
         int32_t prev = -1;
         uint32_t dst, start, uid, last = 0u;
@@ -1969,10 +2035,12 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
         }
         if (!fused) write_record(S, H, d, reward, uid, prev, v, dst, start, -1, PRISMA_ST_PENDING, o, ttl);
         if (S.mem) TP1(4);
+        TP2(4);
         return 1;
     }
     wire_pop(S, R, H, l, k);
     if (S.mem) TP1(5);
+    TP2(5);
     if (S.ctrl && ent_is_big(x)) {                                  // (only with --signaling and --train)
         const uint32_t bp = t_bpair(S, g_gen(x));
         const uint32_t src = bp_src(bp), dst = bp_dst(bp);
@@ -2044,6 +2112,7 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
     }
     receive_counters(S, R, H, x, false, 0u, l);
     if (S.mem) TP1(6);
+    TP2(6);
     return 0;
 }
 

@@ -20,6 +20,14 @@ constexpr uint32_t K_PING = 0u, K_FLOW = 1u, K_COMPLETE = 2u, K_ARRIVE = 3u;
 //            kernels without the --train / notify_dest paths (which never read
 //            the source back) carry the destination there instead, so an
 //            arrival knows it before the record load returns (r_dst)
+//            The register-resident engine's tunnelled-overlay kernels without
+//            those paths carry what an IP header would instead (rip_make):
+//            bits 2-19 the decision's index mod 2^18, bits 20-23 the live TTL
+//            saturated at 15 (tunnels are at most 8 links long, so a saturated
+//            TTL cannot expire inside one), bits 24-31 the tunnel's target
+//            node: a switch inside the tunnel forwards the packet without the
+//            record load (the host picks the other kernels when log_capacity
+//            exceeds 2^18)
 //   T_FRESH  data packet of a flow app on its access link: bits 2-9 its
 //            destination, bit 10 parity of the start second, bits 11-31 uid
 //            mod 2^21 (its source is the switch it arrives at)
@@ -59,6 +67,13 @@ __host__ __device__ inline uint32_t r_make(uint32_t dec, uint32_t src) {
 __host__ __device__ inline uint32_t r_dec(uint32_t x) { return (x >> 2) & ((1u << 22) - 1u); }
 __host__ __device__ inline uint32_t r_src(uint32_t x) { return x >> 24; }
 __host__ __device__ inline uint32_t r_dst(uint32_t x) { return x >> 24; }   // (memory-resident, no ctrl)
+constexpr uint32_t kRipDecBits = 18u, kRipMask = (1u << kRipDecBits) - 1u, kRipTtlSat = 15u;
+__host__ __device__ inline uint32_t rip_make(uint32_t dec, uint32_t ttl, uint32_t tgt) {
+    return T_RELAY | ((dec & kRipMask) << 2) | ((ttl < kRipTtlSat ? ttl : kRipTtlSat) << 20) | (tgt << 24);
+}
+__host__ __device__ inline uint32_t rip_dec(uint32_t x) { return (x >> 2) & kRipMask; }
+__host__ __device__ inline uint32_t rip_ttl(uint32_t x) { return (x >> 20) & 15u; }
+__host__ __device__ inline uint32_t rip_tgt(uint32_t x) { return x >> 24; }
 __host__ __device__ inline uint32_t f_make(uint32_t dst, uint32_t start_parity, uint32_t uid) {
     return T_FRESH | (dst << 2) | (start_parity << 10) | (uid << 11);
 }

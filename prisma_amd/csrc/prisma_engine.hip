@@ -1023,8 +1023,9 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
         e->k_step_mlp = prisma_mem_kernel(2, ctrl);
     } else {
         // the --train echo and notify_dest paths (and the ns-3 streams) are compiled only into the
-        // instances that need them
-        const bool ctrl = L.train || L.notify_dest || L.rng_mode;
+        // instances that need them; the tunnelled-overlay instances without them carry an 18-bit
+        // decision index in relay entries (engine_layout.h rip_make), so a larger log takes the others
+        const bool ctrl = L.train || L.notify_dest || L.rng_mode || (L.tunnels && L.log_cap > (1u << kRipDecBits));
         auto pick = ctrl ? pick_step_ctrl : prisma_pick_step_lite;
         auto pick_mlp = ctrl ? prisma_pick_step_ctrl_mlp : prisma_pick_step_lite_mlp;
         e->k_step = pick(L.FS, L.LS, L.tunnels != 0u);

@@ -225,7 +225,12 @@ class PrismaEngine:
         # notify_dest paths are compiled in (step_kernel.h)
         pl = plan(topo, params)
         self.engine_kind = pl["engine"]
-        ctrl = "true" if (params.get("train") or params.get("notify_dest") or params.get("rng_mode")) else "false"
+        # (tunnelled overlays with a log beyond 2^18 decisions also run the CTRL instances: their
+        # relay entries keep the 22-bit decision index, engine_layout.h rip_make)
+        big_log_tun = (not topo.identity and self.engine_kind != PRISMA_ENGINE_MEMORY
+                       and int(params.get("log_capacity", 8192)) > (1 << 18))
+        ctrl = "true" if (params.get("train") or params.get("notify_dest") or params.get("rng_mode")
+                          or big_log_tun) else "false"
         if self.engine_kind == PRISMA_ENGINE_MEMORY:
             self.kernel_name = f"prisma_mem_step_kernel<false, {ctrl}>"
             self.kernel_name_mlp = f"prisma_mem_step_kernel<true, {ctrl}>"

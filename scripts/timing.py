@@ -97,7 +97,10 @@ if buf[20]:
     for i, nm in enumerate(["flow:record+block", "flow:send", "flow:draw", "flow:tree"]):
         print(f"  {nm:17s} cyc/flow={buf[20 + i] / max(1, nf):8.0f}")
 # fine probes TP(i) (engine_core.h): cycles since the previous probe, per execution
-PROBES = (["arr:record", "arr:issue-prev+obs", "arr:wire-pop+tree", "arr:prev-wait", "arr:data-rest",
+PROBES_2 = ["arr:link+entry", "arr:record-issue+obs", "arr:wire-pop", "arr:prev-wait", "arr:data-rest",
+            "arr:ctl-pop", "arr:ctl-rest", "dec:rows+src", "dec:send", "dec:record", "dec:counters",
+            "cmp:link-get", "cmp:transmit", "cmp:put", "flow:draw+src", "flow:send"]
+PROBES = PROBES_2 if os.environ.get("PRISMA_TP_SET") == "2" else (["arr:record", "arr:issue-prev+obs", "arr:wire-pop+tree", "arr:prev-wait", "arr:data-rest",
            "arr:ctl-pop", "arr:ctl-rest", "cmp:record", "cmp:ring", "cmp:transmit", "cmp:put+tree",
            "flowsend:admit", "flowsend:ring", "flowsend:transmit", "put:store", "put:tree"] if os.environ.get("PRISMA_TP_SET") == "1" else
           ["mlp:wait-arrival", "mlp:sum", "mlp:w3-issue", "mlp:var", "mlp:w4-issue", "mlp:den+xn",
