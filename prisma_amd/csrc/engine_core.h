@@ -317,6 +317,7 @@ struct Sim {
     uint32_t* obs;
     uint32_t* wt; uint32_t* wseq;           // wire: arrival time (low 32 bits) and seq
     uint32_t* went;                         // tunnelled overlays: wire packet entries (LDS)
+    uint32_t* qwin;                         // ... and the FIFO windows of relay_ip kernels (LDS, q_put)
     uint32_t* ring;                         // link FIFOs: LDS, or HBM (tunnelled / memory-resident)
     float* win;
     float* pbd;                             // ping-back delays [responder slot][PBK]
@@ -370,6 +371,7 @@ __device__ inline void sim_bind(Sim& S, const LV& L, unsigned char* lds, const u
     S.wt = (uint32_t*)(lds + L.s_wt());
     S.wseq = (uint32_t*)(lds + L.s_wseq());
     S.went = S.wseq + (uint32_t)L.L() * (uint32_t)L.WCAP();
+    S.qwin = S.went + (uint32_t)L.L() * (uint32_t)L.WCAP();
     S.ring = (uint32_t*)(lds + L.s_ring());
     S.win = (float*)(lds + L.s_win());
     S.pbd = (float*)(lds + L.s_pbd());
@@ -432,6 +434,34 @@ __device__ __forceinline__ void st_rep(const Sim& S, T* p, T v) {
 // a dequeue behind a busy transmitter reads the ring back).
 __device__ __forceinline__ void ring_put(const Sim& S, uint32_t i, uint32_t e) {
     S.ring[i] = e;
+}
+
+// Relay entries carry (decision, live TTL, tunnel target) -- rip_make, engine_layout.h -- in the
+// register-resident engine's tunnelled-overlay kernels without the --train / notify_dest paths
+// (a compile-time constant): a switch inside a tunnel forwards a data packet on its entry alone,
+// as IpForward does on the IP header (ipv4-l3-protocol.cc IpForward), instead of reading the
+// deciding node, action and TTL back from the decision record in HBM.
+__device__ __forceinline__ bool relay_ip(const Sim& S) { return S.tun && !S.mem && !S.ctrl; }
+
+// The same kernels keep the first kQWin packets queued behind each link's busy transmitter -- the
+// ones its next completions dequeue -- in an LDS window, slot = ring index mod kQWin, stored
+// complemented (0 = empty; none of these kernels' entries is all ones); a packet with kQWin or
+// more queued ahead of it goes to the HBM ring.  A dequeue finds the queue head in its window slot
+// iff it was stored there: any later packet for that slot would have had kQWin packets ahead of it
+// (ring capacities are multiples of kQWin, so indices stay consecutive across the wrap).  Their
+// FIFOs had read every dequeued packet back from HBM, most of the time after the line had left L2.
+__device__ __forceinline__ void q_put(const Sim& S, uint32_t l, uint32_t off, uint32_t idx, uint32_t ahead,
+                                      uint32_t e) {
+    if (relay_ip(S) && ahead < kQWin) S.qwin[l * kQWin + (idx & (kQWin - 1u))] = ~e;
+    else ring_put(S, off + idx, e);
+}
+__device__ __forceinline__ uint32_t q_take(const Sim& S, uint32_t l, uint32_t off, uint32_t idx) {
+    if (relay_ip(S)) {
+        uint32_t* w = &S.qwin[l * kQWin + (idx & (kQWin - 1u))];
+        const uint32_t v = rfl(*w);
+        if (v != 0u) { *w = 0u; return ~v; }
+    }
+    return rfl(S.ring[off + idx]);
 }
 
 // uniform LDS reads (every lane reads the same address: broadcast, no conflict)
@@ -765,14 +795,14 @@ __device__ __forceinline__ int link_send_k(const Sim& S, RS& R, Hot& H, uint32_t
     }
     uint32_t cap = ring_cap(S, l), off = ring_off(S, l);
     if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
-    if (ring_store_needed(S, k)) ring_put(S, off + k.tail, e);
+    if (ring_store_needed(S, k)) q_put(S, l, off, k.tail, k.n_queue, e);
     k.tail = (k.tail + 1 == cap) ? 0 : k.tail + 1;
     k.n_queue++;
     k.qb += size;
     TP1(12);
     if (!k.busy) {                                              // :643-650
         uint32_t xi = k.txp;
-        uint32_t hx = (k.n_queue == 1) ? e : u_ld32(&S.ring[off + xi]);
+        uint32_t hx = (k.n_queue == 1) ? e : q_take(S, l, off, xi);
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
@@ -807,13 +837,13 @@ __device__ __forceinline__ int link_send(const Sim& S, RS& R, Hot& H, uint32_t l
     }
     uint32_t cap = ring_cap(S, l), off = ring_off(S, l);
     if (k.n_wire + k.n_queue + 1u > cap) { fail(H, PRISMA_EBIT_RING); return 0; }
-    if (ring_store_needed(S, k)) ring_put(S, off + k.tail, e);
+    if (ring_store_needed(S, k)) q_put(S, l, off, k.tail, k.n_queue, e);
     k.tail = (k.tail + 1 == cap) ? 0 : k.tail + 1;
     k.n_queue++;
     k.qb += size;
     if (!k.busy) {                                              // :643-650
         uint32_t xi = k.txp;
-        uint32_t hx = (k.n_queue == 1) ? e : u_ld32(&S.ring[off + xi]);
+        uint32_t hx = (k.n_queue == 1) ? e : q_take(S, l, off, xi);
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
         k.n_wire++;
@@ -837,7 +867,7 @@ __device__ __forceinline__ void on_complete(const Sim& S, RS& R, Hot& H, uint32_
     if (k.n_queue) {
         uint32_t cap = ring_cap(S, l);
         uint32_t xi = k.txp;
-        uint32_t hx = u_ld32(&S.ring[ring_off(S, l) + xi]);
+        uint32_t hx = q_take(S, l, ring_off(S, l), xi);
         if (S.mem) TP1(8);
         k.txp = (xi + 1 == cap) ? 0 : xi + 1;
         k.n_queue--;
@@ -1005,12 +1035,7 @@ __device__ __forceinline__ uint32_t tunnel_link(const Sim& S, uint32_t t) {
     return S.tun ? ti_link(S.T->tinfo[t]) : t;
 }
 
-// Relay entries carry (decision, live TTL, tunnel target) -- rip_make, engine_layout.h -- in the
-// register-resident engine's tunnelled-overlay kernels without the --train / notify_dest paths
-// (a compile-time constant): a switch inside a tunnel forwards a data packet on its entry alone,
-// as IpForward does on the IP header (ipv4-l3-protocol.cc IpForward), instead of reading the
-// deciding node, action and TTL back from the decision record in HBM.
-__device__ __forceinline__ bool relay_ip(const Sim& S) { return S.tun && !S.mem && !S.ctrl; }
+// (relay_ip: ring_put)
 __device__ __forceinline__ uint32_t relay_dist(const Sim& S, uint32_t d, uint32_t x) {
     return relay_ip(S) ? (d - rip_dec(x)) & kRipMask : (d - r_dec(x)) & kRelayMask;
 }

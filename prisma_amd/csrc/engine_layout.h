@@ -67,6 +67,9 @@ __host__ __device__ inline uint32_t r_make(uint32_t dec, uint32_t src) {
 __host__ __device__ inline uint32_t r_dec(uint32_t x) { return (x >> 2) & ((1u << 22) - 1u); }
 __host__ __device__ inline uint32_t r_src(uint32_t x) { return x >> 24; }
 __host__ __device__ inline uint32_t r_dst(uint32_t x) { return x >> 24; }   // (memory-resident, no ctrl)
+// FIFO window of the same kernels: the first kQWin packets queued behind a busy transmitter of
+// each link sit in LDS (Layout: after the wire-slot entries), the rest in the HBM ring
+constexpr uint32_t kQWin = 4u;
 constexpr uint32_t kRipDecBits = 18u, kRipMask = (1u << kRipDecBits) - 1u, kRipTtlSat = 15u;
 __host__ __device__ inline uint32_t rip_make(uint32_t dec, uint32_t ttl, uint32_t tgt) {
     return T_RELAY | ((dec & kRipMask) << 2) | ((ttl < kRipTtlSat ? ttl : kRipTtlSat) << 20) | (tgt << 24);

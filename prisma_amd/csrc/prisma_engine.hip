@@ -739,9 +739,11 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
         if (L.train)
             for (const auto& pth : OP.epaths)
                 for (size_t i = 0; i < pth.size(); ++i) c[pth[i]] += (double)((uint32_t)((double)(i + 1) * hop_s / tx_s) + 1u);
+        // (multiples of kQWin too: the LDS FIFO windows, engine_core.h q_put)
+        const uint32_t m = (uint32_t)L.WCAP > kQWin ? (uint32_t)L.WCAP : kQWin;
         for (int l = 0; l < E; ++l) {
             uint32_t qs = data_max + (uint32_t)c[l] + (uint32_t)L.WCAP;
-            rcap[l] = (qs + (uint32_t)L.WCAP - 1) / (uint32_t)L.WCAP * (uint32_t)L.WCAP;
+            rcap[l] = (qs + m - 1) / m * m;
         }
         span = 2.0 * (double)OP.plen * hop_s;
     }
@@ -906,7 +908,8 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     // replica, 10 per CU: two rounds for 4 096 replicas) and the packet entry of each wire
     // slot in LDS after the seqs (Sim::went), so an arrival does not read the ring.
     L.s_wt = take(4u * Lk * L.WCAP);
-    L.s_wseq = take(4u * Lk * L.WCAP * (OP.tunnels ? 2u : 1u));
+    // (tunnelled: the wire slots' packet entries, then kQWin FIFO window slots per link, q_put)
+    L.s_wseq = take(4u * Lk * (L.WCAP * (OP.tunnels ? 2u : 1u) + (OP.tunnels ? kQWin : 0u)));
     if (!OP.tunnels) L.s_ring = take(4u * tot);
     L.s_win = take(4u * (uint32_t)OP.T * L.MA);
     L.s_pbd = take(4u * (uint32_t)(OP.tunnels ? OP.n_resp : OP.T) * L.PBK);

@@ -418,6 +418,53 @@ def test_tunnel_ttl_expiry_parity(oracle_mod):
     run_table_both(oracle_mod, topo, params, 3, 10 ** 6, table)
 
 
+def test_tunnel_big_log_parity(oracle_mod):
+    """A log beyond 2^18 decisions on a tunnelled overlay runs the kernels whose relay entries keep
+    the 22-bit decision index (engine_layout.h rip_make; the host's instance pick)."""
+    topo = Topology.example("overlay_full_mesh_3n_abilene", 0, 20.0)
+    params = engine_params(topo, sim_time_s=10.0, ping_as_obs=0, seed=7, log_capacity=1 << 19)
+    eng = PrismaEngine(topo, params, 1)
+    assert eng.kernel_name.endswith("true, true>")            # TUN, CTRL instance
+    eng.close()
+    cnt = run_table_both(oracle_mod, topo, params, 2, 3000, _random_table(topo, 7))
+    assert cnt["ov_lost"].sum() > 0
+
+
+def test_tunnel_external_parity(oracle_mod):
+    """External actions on a tunnelled overlay without the --train / notify_dest paths: each
+    launch opens with the pending decision (finish_pending), whose relay entry takes the TTL from
+    the decision's record."""
+    topo = Topology.example("overlay_full_mesh_3n_abilene", 0, 10.0)
+    params = engine_params(topo, sim_time_s=4.0, ping_as_obs=1)
+    R = 3
+    eng = PrismaEngine(topo, params, R)
+    assert eng.kernel_name.endswith("true, false>")           # TUN, no CTRL: relay entries with the target
+    eng.reset(0)
+    orcs = [oracle_mod.OracleSim(topo, params, replica=r) for r in range(R)]
+    ref_obs = [o.step(-1) for o in orcs]
+    obs, mask, node = eng.step(None)
+    rng = np.random.default_rng(3)
+    for s in range(800):
+        g, m, nd = obs.cpu().numpy(), mask.cpu().numpy(), node.cpu().numpy()
+        acts = np.zeros(R, dtype=np.int32)
+        for r in range(R):
+            assert (ref_obs[r] is None) == (m[r] == 0), (s, r)
+            if ref_obs[r] is None:
+                continue
+            assert np.array_equal(ref_obs[r], g[r]), (s, r, g[r], ref_obs[r])
+            acts[r] = rng.integers(0, topo.degrees[nd[r]])
+        ref_obs = [orcs[r].step(int(acts[r])) if ref_obs[r] is not None else None for r in range(R)]
+        obs, mask, node = eng.step(torch.from_numpy(acts).cuda())
+    torch.cuda.synchronize()
+    cnt = eng.counters()
+    log = eng.log_tensor().cpu().numpy()
+    for r in range(R):
+        ref = orcs[r].records()
+        assert eng.records(r, 0, len(ref), log_host=log).tobytes() == ref.tobytes()
+        assert_counters_equal(cnt[r], orcs[r].counters(), r)
+    eng.close()
+
+
 def test_tunnel_external_notify_train_parity(oracle_mod):
     topo = Topology.example("overlay_full_mesh_3n_abilene", 0, 10.0)
     params = engine_params(topo, sim_time_s=4.0, ping_as_obs=1, notify_dest=1, train=1)
