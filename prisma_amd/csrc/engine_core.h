@@ -918,11 +918,13 @@ __device__ __forceinline__ uint32_t ping_value_lane(double avg, uint32_t lo, dou
 // is tunnel ovrow[v] + a; its queue is that of the tunnel's first link
 // (the device RouteOutput picks, data-packet-manager.cc:180-195), which is
 // the tunnel itself on identity overlays.
+// (r0, deg: node v's row pointer and degree, read by the caller, which hands them on to the
+// decision's send)
 template <int FS, int LS>
 __device__ __forceinline__ uint32_t observe_links(const Sim& S, const Regs<FS, LS>& R, const Hot& H, uint32_t v,
-                                                  double now_s) {
+                                                  double now_s, int r0 = -1, int deg = 0) {
     if (PRISMA_ABLATE & 4) return 0u;
-    const int r0 = t_ovrow(S, v), deg = t_ovrow(S, v + 1) - r0;
+    if (r0 < 0) { r0 = t_ovrow(S, v); deg = t_ovrow(S, v + 1) - r0; }
     const int lane = S.lane;
     uint32_t src = (uint32_t)(r0 + lane - 1);
     const bool pobs = S.lv.ping_as_obs() != 0u;
@@ -1065,11 +1067,13 @@ __device__ __forceinline__ void relay_dropped(const Sim& S, uint32_t dd, uint32_
 // d at node v, then the Receive tail.  x is the arriving entry (for the
 // counters); fused: the record is written here once, with the final status
 // (table policy).
-template <class RS>
+// ROW: r0_in / deg_in hold node v's row pointer and degree (read on the arrival)
+template <bool ROW = false, class RS>
 __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint32_t x, uint32_t dst,
                                                uint32_t start, uint32_t uid, uint32_t v, uint32_t d, int action,
                                                bool fused, double reward, int32_t prev, uint32_t obs_reg,
-                                               uint32_t echo_link, uint32_t last, uint32_t ttl) {
+                                               uint32_t echo_link, uint32_t last, uint32_t ttl,
+                                               int r0_in = -1, int deg_in = 0) {
     const LV& L = S.lv;
 #if PRISMA_TIMING
     S.tlast = TM_NOW();
@@ -1078,7 +1082,8 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
     if (echo_link != kNoLink) send_echo(S, R, H, echo_link, uid, last);
     TP2_START();
     v = rfl(v);                                     // (scalar loads of the row pointers)
-    int r0 = t_ovrow(S, v), deg = t_ovrow(S, v + 1) - r0;
+    int r0 = r0_in, deg = deg_in;
+    if (!ROW) { r0 = t_ovrow(S, v); deg = t_ovrow(S, v + 1) - r0; }
     uint32_t status;
     if ((uint32_t)action < (uint32_t)deg) {                      // 0 <= action < deg
         const uint32_t tiw = S.tun ? (uint32_t)S.T->tinfo[(uint32_t)(r0 + action)] : 0u;
@@ -1839,6 +1844,7 @@ __device__ __forceinline__ void wire_pop(const Sim& S, RS& R, const Hot& H, uint
 
 struct Decision {
     uint32_t x, dst, start, uid, v, d; double reward; int32_t prev; uint32_t obs, flags, last, ttl;
+    int32_t r0, deg;             // register-resident engine: node v's row pointer and degree (r0 < 0: not read)
 };
 
 // a control packet (or a data packet inside a tunnel) continues along the
@@ -2011,7 +2017,10 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
             ttl = ttl_prev - (ti_len(ti) - 1u);
         }
         H.dec = d + 1u;
-        const uint32_t obs_links = S.mem ? obs_early : observe_links(S, R, H, v, ns_to_sec(H.now));
+        int r0 = -1, deg = 0;
+        if (!S.mem) { r0 = t_ovrow(S, v); deg = t_ovrow(S, v + 1) - r0; }
+        const uint32_t obs_links = S.mem ? obs_early : observe_links(S, R, H, v, ns_to_sec(H.now), r0, deg);
+        D.r0 = r0; D.deg = deg;
         const int64_t t_prev = mk64(rfl(ph.x), rfl(ph.y));
         const uint32_t uid_prev = rfl(ph.z), w_prev = rfl(pw.x);
         if (S.mem) TP1(3);
@@ -2518,6 +2527,7 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
         TM_MARK(0);
         if (kind == K_ARRIVE) {
             Decision D;
+            D.r0 = -1; D.deg = 0;
             MlpPre1 Mp;                                  // (kPre) the decision's first weights, fetched on arrival
             const int need = on_arrive<kPre>(S, R, H, id, D, table_mode, Mp);
             TM_MARK(1);
@@ -2525,9 +2535,12 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
                 if (table_mode) {
                     const int a = mlp_mode ? mlp_action<MB, kPre>(S, D.v, D.obs, Mp)
                                            : table_action(S, D.v * NN + D.dst);
-                    apply_decision(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, a, true,
+                    // (the row handoff: headline +2.1 % in A/B; config 4's MLP instance -2 %, so
+                    // the MLP instances read the row again)
+                    apply_decision<!RS::kMem && !MLP>(S, R, H, D.x, D.dst, D.start, D.uid, D.v, D.d, a, true,
                                    D.reward, D.prev, D.obs,
-                                   (D.flags & PEND_ECHO) ? (uint32_t)t_lrev(S, id) : kNoLink, D.last, D.ttl);
+                                   (D.flags & PEND_ECHO) ? (uint32_t)t_lrev(S, id) : kNoLink, D.last, D.ttl,
+                                   D.r0, D.deg);
                     H.hops_launch++;
                     if (H.hops_launch >= max_hops) H.stop = 1;
                     TM_MARK(2);

@@ -371,8 +371,9 @@ __device__ __forceinline__ void lazy_resolve(const Sim& S, MemSt& R, Hot& H, boo
 
 // observation of node v: lane i (1 <= i <= deg) gathers the words of link ovrow[v] + i - 1
 // (written by other lanes of this wave in earlier events)
+// (the row pointer and degree arguments of the register-resident engine's version: not taken)
 __device__ __forceinline__ uint32_t observe_links(const Sim& S, const MemSt& R, const Hot& H, uint32_t v,
-                                                  double now_s) {
+                                                  double now_s, int = -1, int = 0) {
     const int r0 = t_ovrow(S, v), deg = t_ovrow(S, v + 1) - r0;
     const int lane = S.lane;
     if (lane < 1 || lane > deg) return 0u;
