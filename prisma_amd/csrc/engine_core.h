@@ -1088,8 +1088,10 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
     if ((uint32_t)action < (uint32_t)deg) {                      // 0 <= action < deg
         const uint32_t tiw = S.tun ? (uint32_t)S.T->tinfo[(uint32_t)(r0 + action)] : 0u;
         const uint32_t l = S.tun ? ti_link(tiw) : (uint32_t)(r0 + action);   // RouteOutput (:281-287)
-        CNT_ADD(S, hops, 1u);
-        CNT_ADD(S, hop_deg_sum, (uint64_t)deg);
+        if (RS::kMem || S.mlp_inst) {
+            CNT_ADD(S, hops, 1u);
+            CNT_ADD(S, hop_deg_sum, (uint64_t)deg);
+        }
         // (memory-resident engine without the ctrl paths: the destination instead of the
         // source, engine_layout.h)
         const uint32_t src = (RS::kMem && !S.ctrl) ? dst : ent_src(x, v);
@@ -1116,7 +1118,21 @@ __device__ __forceinline__ void apply_decision(const Sim& S, RS& R, Hot& H, uint
     if (fused) write_record(S, H, d, reward, uid, prev, v, dst, start, action, status, obs_reg, ttl);
     else patch_record(S, H, d, action, status);
     TP2(9);
-    receive_counters(S, R, H, x, false, 0u, 0u);
+    if (RS::kMem || S.mlp_inst) {
+        receive_counters(S, R, H, x, false, 0u, 0u);
+    } else if (S.lane == 0) {
+        // table instances: the hop's integer counters and the Receive tail's (a data packet:
+        // receive_counters) in one lane-0 region -- integer adds, so their order is free (A/B:
+        // headline +0.7 %)
+        if ((uint32_t)action < (uint32_t)deg) {
+            lds_add(&S.c->hops, (decltype(S.c->hops))1u);
+            lds_add(&S.c->hop_deg_sum, (decltype(S.c->hop_deg_sum))deg);
+        }
+        if (ent_type(x) == T_FRESH) {
+            lds_add(&S.c->ov_injected, (decltype(S.c->ov_injected))1u);
+            lds_add(&S.c->bytes_data, (decltype(S.c->bytes_data))(L.data_size() - 2u));
+        }
+    }
     TP2(10);
 #if PRISMA_TIMING
     { const uint64_t t = TM_NOW(); S.tsub[1] += t - S.tlast; S.tlast = t; }
