@@ -186,7 +186,16 @@ def cpu_baseline(topo, params, kind: str, policy, hops_per_thread: int, hops_1co
         def run(sim, n):
             return sim.run_table(pol, n) if kind == "table" else sim.run_mlp(pol, n)
 
+        errs = []
+
         def work(i):
+            try:
+                body(i)
+            except BaseException as exc:            # a failed worker releases the others
+                errs.append(exc)
+                bar.abort()
+
+        def body(i):
             ep = 0
             sims[i] = O.OracleSim(topo, params, replica=100000 + i, episode=ep)
             w = 0
@@ -211,12 +220,17 @@ def cpu_baseline(topo, params, kind: str, policy, hops_per_thread: int, hops_1co
         ths = [threading.Thread(target=work, args=(i,)) for i in range(n_threads)]
         for t in ths:
             t.start()
-        bar.wait()                                  # every thread built (and warmed) its replica
-        t0 = time.perf_counter()
-        bar.wait()
-        dt = time.perf_counter() - t0
+        try:
+            bar.wait()                              # every thread built (and warmed) its replica
+            t0 = time.perf_counter()
+            bar.wait()
+            dt = time.perf_counter() - t0
+        except threading.BrokenBarrierError:
+            dt = None
         for t in ths:
             t.join()
+        if errs or dt is None:
+            raise RuntimeError(f"cpu_baseline worker failed: {errs[0] if errs else 'barrier broken'}")
         return int(sum(done)), int(sum(episodes)), dt
 
     h1, e1, d1 = timed(1, hops_1core)

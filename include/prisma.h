@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define PRISMA_ABI_VERSION 9
+#define PRISMA_ABI_VERSION 10
 
 /* status codes */
 #define PRISMA_OK              0
@@ -369,6 +369,27 @@ int prisma_compact_pending(prisma_env_t* env, const uint8_t* mask, const int32_t
 int prisma_expand_actions(prisma_env_t* env, const int32_t* ids, const int32_t* count,
                           const int32_t* packed_actions, int32_t fill, int32_t* actions_out,
                           void* stream);
+
+/* The step-kernel instances prisma_create picked for this env (ABI 10), as
+ * the library decided, for profiles and tests (the demangled kernel name is
+ * prisma_step_kernel_t<flow_slots, link_slots, MLP, tunnels, ctrl> on the
+ * register engine, prisma_mem_step_kernel<MLP, ctrl> on the memory engine). */
+typedef struct prisma_kernel_info {
+    uint32_t engine;            /* PRISMA_ENGINE_REGISTER or _MEMORY       */
+    int32_t  flow_slots;        /* template slots (register engine; else 0) */
+    int32_t  link_slots;
+    uint32_t tunnels;           /* tunnelled-overlay instances              */
+    uint32_t ctrl;              /* --train / notify_dest / ns-3 stream paths
+                                   compiled in (also: tunnelled overlays with
+                                   log_capacity >= 2^18)                    */
+    uint32_t relay_ip;          /* relay entries carry (decision, TTL, tunnel
+                                   target) and FIFO windows sit in LDS       */
+    uint32_t relay_dec_bits;    /* decision-index bits of a relay entry (18
+                                   with relay_ip, 22 otherwise; 0 without
+                                   tunnels): the log-wrap check sees ages up
+                                   to 2^bits                               */
+} prisma_kernel_info_t;
+int prisma_kernel_info(prisma_env_t* env, prisma_kernel_info_t* out);
 
 /* Bytes of per-replica state (the LDS image) and LDS bytes per workgroup. */
 int prisma_state_bytes(prisma_env_t* env, uint32_t* state_bytes,

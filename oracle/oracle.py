@@ -80,6 +80,7 @@ def lib():
         L.or_copy_records.restype = C.c_int64
         L.or_copy_records.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p]
         L.or_counters.argtypes = [C.c_void_p, C.c_void_p]
+        L.or_diag.argtypes = [C.c_void_p, C.c_void_p]
         L.or_enable_trace.argtypes = [C.c_void_p, C.c_int]
         L.or_trace_count.restype = C.c_int64
         L.or_trace_count.argtypes = [C.c_void_p]
@@ -215,6 +216,12 @@ class OracleSim:
         out = np.zeros(1, dtype=self.cnt_dtype)
         lib().or_counters(self.h, out.ctypes.data)
         return out[0]
+
+    def diag(self) -> dict:
+        """Test diagnostics (or_diag): drops inside tunnels, FIFO depths now."""
+        out = np.zeros(4, dtype=np.int64)
+        lib().or_diag(self.h, out.ctypes.data)
+        return dict(relay_drops=int(out[0]), max_queue=int(out[1]), queued=int(out[2]), deep_fifos=int(out[3]))
 
     def enable_trace(self, on: bool = True):
         lib().or_enable_trace(self.h, int(on))

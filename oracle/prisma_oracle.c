@@ -285,6 +285,8 @@ struct or_sim {
     int trace_on; int64_t* tr; int64_t tr_n, tr_cap;
     /* last info string */
     char info[4096];
+    /* test diagnostics (or_diag): data packets dropped on a FIFO inside a tunnel */
+    int64_t relay_drops;
 };
 
 static void* xrealloc(void* p, size_t n) {
@@ -463,6 +465,7 @@ static int dev_send(or_sim_t* s, int di, int p) {                   /* :595-666 
         return 1;
     }
     if (k->type == DATA_PACKET) {                                    /* :655-664 */
+        if (!d->is_access && k->last_hop != d->from_node) s->relay_drops++;
         if (k->valable && k->dst != d->from_node) {
             s->cnt.ov_lost++;
             add_loss_penalty_to_cost(s);
@@ -1237,6 +1240,20 @@ void or_counters(const or_sim_t* s, void* out) {
     c.hops_total = c.hops;
     c.events_total = c.events;
     memcpy(out, &c, sizeof(c));
+}
+
+void or_diag(const or_sim_t* s, int64_t out[4]) {
+    int64_t mx = 0, tot = 0, deep = 0;
+    for (int i = 0; i < s->E; ++i) {               /* switch devices: the FIFOs a test probes */
+        const int n = s->dev[i].q_len;
+        if (n > mx) mx = n;
+        tot += n;
+        if (n > 4) deep++;
+    }
+    out[0] = s->relay_drops;
+    out[1] = mx;
+    out[2] = tot;
+    out[3] = deep;
 }
 
 void or_enable_trace(or_sim_t* s, int on) { s->trace_on = on; }

@@ -108,6 +108,12 @@ int64_t or_copy_records(const or_sim_t* s, int64_t first, int64_t count, void* o
 /* Counters with the same byte layout as prisma_counters_t. */
 void or_counters(const or_sim_t* s, void* out);
 
+/* Test diagnostics: out[0] data packets dropped on a FIFO inside a tunnel (not the deciding
+ * node's first link), out[1] the longest switch FIFO now (packets waiting, excluding the one in
+ * transmission), out[2] packets waiting in all switch FIFOs, out[3] switch FIFOs with more than
+ * 4 waiting (deeper than the engine's LDS FIFO window, so part of them sits in the HBM ring). */
+void or_diag(const or_sim_t* s, int64_t out[4]);
+
 /* Optional event trace: (t_ns, seq, kind, id) per executed event. */
 void    or_enable_trace(or_sim_t* s, int on);
 int64_t or_trace_count(const or_sim_t* s);

@@ -264,6 +264,7 @@ struct prisma_env {
     float* d_mlp_rp = nullptr;           // interleaved DQN-buffer layers 2-4 (prisma_run, mode 4)
     unsigned char* d_spare = nullptr;    // next-episode images (register engine with auto_reset)
     uint32_t* d_rng = nullptr;           // ns-3 stream table (PRISMA_RNG_NS3, engine_layout.h kMrgPowers)
+    prisma_kernel_info_t kinfo{};        // the step-kernel instances prisma_create picked
     bool reset_done = false;
 };
 
@@ -1027,14 +1028,24 @@ extern "C" int prisma_create(const prisma_topology_t* topo, const prisma_params_
     } else {
         // the --train echo and notify_dest paths (and the ns-3 streams) are compiled only into the
         // instances that need them; the tunnelled-overlay instances without them carry an 18-bit
-        // decision index in relay entries (engine_layout.h rip_make), so a larger log takes the others
-        const bool ctrl = L.train || L.notify_dest || L.rng_mode || (L.tunnels && L.log_cap > (1u << kRipDecBits));
+        // decision index in relay entries (engine_layout.h rip_make).  Their wrap check (a relay
+        // entry older than the log, PRISMA_EBIT_LOGWRAP) needs log ages up to log_cap to stay below
+        // 2^18, so a log of 2^18 records or more takes the others (22-bit index)
+        const bool ctrl = L.train || L.notify_dest || L.rng_mode || (L.tunnels && L.log_cap >= (1u << kRipDecBits));
         auto pick = ctrl ? pick_step_ctrl : prisma_pick_step_lite;
         auto pick_mlp = ctrl ? prisma_pick_step_ctrl_mlp : prisma_pick_step_lite_mlp;
         e->k_step = pick(L.FS, L.LS, L.tunnels != 0u);
         e->k_reset = pick_reset(L.FS, L.LS);
         e->k_step_mlp = pick_mlp(L.FS, L.LS, L.tunnels != 0u);
+        e->kinfo.ctrl = ctrl ? 1u : 0u;
+        e->kinfo.relay_ip = (L.tunnels && !ctrl) ? 1u : 0u;
+        e->kinfo.relay_dec_bits = L.tunnels ? (ctrl ? 22u : kRipDecBits) : 0u;
     }
+    e->kinfo.engine = L.mem ? PRISMA_ENGINE_MEMORY : PRISMA_ENGINE_REGISTER;
+    e->kinfo.flow_slots = L.mem ? 0 : L.FS;
+    e->kinfo.link_slots = L.mem ? 0 : L.LS;
+    e->kinfo.tunnels = L.tunnels ? 1u : 0u;
+    if (L.mem) e->kinfo.ctrl = (L.train || L.notify_dest || L.rng_mode) ? 1u : 0u;
     (void)hipFuncSetAttribute(e->k_step_mlp, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_mlp_bytes);
     (void)hipFuncSetAttribute(e->k_step, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
     (void)hipFuncSetAttribute(e->k_reset, hipFuncAttributeMaxDynamicSharedMemorySize, (int)L.lds_bytes);
@@ -1217,6 +1228,12 @@ extern "C" int prisma_expand_actions(prisma_env_t* e, const int32_t* ids, const 
                        packed_actions, e->R, fill, actions_out);
     hipError_t err = hipGetLastError();
     if (err != hipSuccess) return set_err(PRISMA_ERR_LAUNCH, std::string("expand launch failed: ") + hipGetErrorString(err));
+    return PRISMA_OK;
+}
+
+extern "C" int prisma_kernel_info(prisma_env_t* e, prisma_kernel_info_t* out) {
+    if (!e || !out) return set_err(PRISMA_ERR_ARG, "null argument");
+    *out = e->kinfo;
     return PRISMA_OK;
 }
 

@@ -54,8 +54,14 @@ prisma_step_kernel_t(KParams P) {
         const KParams* kp = (const KParams*)__builtin_amdgcn_kernarg_segment_ptr();
         asm volatile("" : "+s"(kp));
         const KParams P2 = *kp;
-        if (spare_restart(P2, S, R, r, done, budget))
+        if (spare_restart(P2, S, R, r, done, budget)) {
             event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P2, S, R, r, budget);
+            // stage out from the reloaded arguments too: with P's pointers kept live across this
+            // loop the headline instance spilled 7 VGPRs and reloaded them inside it (round 6:
+            // 128 VGPRs + 32 B scratch -> 123 VGPRs, no scratch)
+            stage_out(lds, P2, r, lane, R);
+            return;
+        }
     }
     stage_out(lds, P, r, lane, R);
 }

@@ -18,7 +18,7 @@ from .topology import Topology
 
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libprisma_amd.so")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 PRISMA_POLICY_TABLE = 1
 PRISMA_POLICY_DQN_BUFFER = 2
 PRISMA_ENGINE_AUTO, PRISMA_ENGINE_REGISTER, PRISMA_ENGINE_MEMORY = 0, 1, 2
@@ -65,6 +65,12 @@ class _LogView(C.Structure):
                 ("obs_width", C.c_int32), ("n_replicas", C.c_int32)]
 
 
+class _KernelInfo(C.Structure):
+    _fields_ = [("engine", C.c_uint32), ("flow_slots", C.c_int32), ("link_slots", C.c_int32),
+                ("tunnels", C.c_uint32), ("ctrl", C.c_uint32), ("relay_ip", C.c_uint32),
+                ("relay_dec_bits", C.c_uint32)]
+
+
 class _Plan(C.Structure):
     _fields_ = [("state_bytes", C.c_uint32), ("lds_bytes", C.c_uint32), ("lds_state_bytes", C.c_uint32),
                 ("ring_entries", C.c_uint32), ("record_bytes", C.c_uint32), ("obs_width", C.c_int32),
@@ -75,7 +81,7 @@ EXPORTS = [
     "prisma_abi_version", "prisma_last_error", "prisma_build_id", "prisma_create", "prisma_reset", "prisma_step", "prisma_run",
     "prisma_read_counters", "prisma_counters_device", "prisma_log_view", "prisma_copy_log",
     "prisma_copy_counters", "prisma_gather_records", "prisma_state_bytes", "prisma_plan", "prisma_destroy",
-    "prisma_compact_pending", "prisma_expand_actions",
+    "prisma_compact_pending", "prisma_expand_actions", "prisma_kernel_info",
 ]
 
 _lib = None
@@ -128,6 +134,8 @@ def load_library(path: str = None):
     L.prisma_expand_actions.restype = C.c_int
     L.prisma_expand_actions.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p,
                                         C.c_void_p]
+    L.prisma_kernel_info.restype = C.c_int
+    L.prisma_kernel_info.argtypes = [C.c_void_p, C.POINTER(_KernelInfo)]
     L.prisma_state_bytes.restype = C.c_int
     L.prisma_state_bytes.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
     L.prisma_plan.restype = C.c_int
@@ -220,29 +228,30 @@ class PrismaEngine:
         sb, lb = C.c_uint32(), C.c_uint32()
         _check(L.prisma_state_bytes(self.h, C.byref(sb), C.byref(lb)))
         self.state_bytes, self.lds_bytes = int(sb.value), int(lb.value)
-        # step-kernel instance the library picked (demangled name, for profiles): the register
-        # slots come from prisma_plan; the last template argument says whether the --train echo /
-        # notify_dest paths are compiled in (step_kernel.h)
-        pl = plan(topo, params)
-        self.engine_kind = pl["engine"]
-        # (tunnelled overlays with a log beyond 2^18 decisions also run the CTRL instances: their
-        # relay entries keep the 22-bit decision index, engine_layout.h rip_make)
-        big_log_tun = (not topo.identity and self.engine_kind != PRISMA_ENGINE_MEMORY
-                       and int(params.get("log_capacity", 8192)) > (1 << 18))
-        ctrl = "true" if (params.get("train") or params.get("notify_dest") or params.get("rng_mode")
-                          or big_log_tun) else "false"
+        # step-kernel instances the library picked (prisma_kernel_info: the choice prisma_create
+        # made, reported by the library; the demangled names are for profiles)
+        ki = self.kernel_info()
+        self.engine_kind = ki["engine"]
+        ctrl = "true" if ki["ctrl"] else "false"
         if self.engine_kind == PRISMA_ENGINE_MEMORY:
             self.kernel_name = f"prisma_mem_step_kernel<false, {ctrl}>"
             self.kernel_name_mlp = f"prisma_mem_step_kernel<true, {ctrl}>"
         else:
-            fs, ls = pl["flow_slots"], pl["link_slots"]
-            tun = "false" if topo.identity else "true"
+            fs, ls = ki["flow_slots"], ki["link_slots"]
+            tun = "true" if ki["tunnels"] else "false"
             # template arguments: slots, in-kernel MLP, tunnels, --train/notify_dest paths
             self.kernel_name = f"prisma_step_kernel_t<{fs}, {ls}, false, {tun}, {ctrl}>"
             self.kernel_name_mlp = f"prisma_step_kernel_t<{fs}, {ls}, true, {tun}, {ctrl}>"
         self.obs = torch.zeros((self.R, self.W), dtype=torch.int32, device=self.torch_device)
         self.mask = torch.zeros(self.R, dtype=torch.uint8, device=self.torch_device)
         self.node = torch.zeros(self.R, dtype=torch.int32, device=self.torch_device)
+
+    def kernel_info(self) -> dict:
+        """prisma_kernel_info: the step-kernel instances this engine launches (engine, template
+        slots, tunnels, ctrl paths, relay entries with LDS FIFO windows, relay index bits)."""
+        ki = _KernelInfo()
+        _check(_lib.prisma_kernel_info(self.h, C.byref(ki)))
+        return {k: int(getattr(ki, k)) for k, _ in _KernelInfo._fields_}
 
     # -- lifecycle --------------------------------------------------------
     def close(self):
@@ -301,10 +310,10 @@ class PrismaEngine:
                 and ids.dtype == torch.int32):
             cnt = self._ccount
         else:
-            if not hasattr(self, "_ecount"):
-                self._ecount = torch.zeros(1, dtype=torch.int32, device=self.torch_device)
-            cnt = self._ecount
-            cnt.fill_(n)
+            # a fresh count per call, filled on the launch's own stream: a reused buffer could be
+            # refilled while an earlier expand still reads it, or read before a fill on another stream
+            with torch.cuda.stream(stream if stream is not None else torch.cuda.current_stream()):
+                cnt = torch.full((1,), n, dtype=torch.int32, device=self.torch_device)
         # (an empty batch still passes valid device pointers: the count says there is nothing)
         ids_c = ids.to(torch.int32).contiguous() if n else torch.zeros(1, dtype=torch.int32, device=self.torch_device)
         act = (packed_actions.to(torch.int32).contiguous() if n

@@ -32,6 +32,7 @@ class OracleChain:
         self.hops_total = 0
         self.events_done = 0                   # events of the finished episodes
         self.t_done = 0                        # simulated ns of the finished episodes
+        self.end_diag = []                     # oracle diagnostics (or_diag) at each episode end
 
     def _run(self, hops):
         kind, pol = self.policy
@@ -40,6 +41,8 @@ class OracleChain:
     def _next_episode(self):
         c = self.o.counters()
         assert int(c["episode_over"]) == 1
+        if hasattr(self.o, "diag"):
+            self.end_diag.append(self.o.diag())
         self.done.append((self.base, self.o, c))
         self.events_done += int(c["events"])
         self.t_done += int(c["now_ns"])
@@ -132,13 +135,17 @@ def check_near_ties(net_cpu, weights_host, checker, recs, rel_tol=1e-5):
 
 
 def compare_steady(oracle_mod, eng, topo, params, policy, *, t_target_s, hops_per_launch, min_episode=0,
-                   replicas=None, net_cpu=None, max_launches=400, label=""):
+                   replicas=None, net_cpu=None, max_launches=400, label="", log_tail=False):
     """Run `eng` launch by launch (fused policy) and compare every new decision record and the
     counters of each checked replica with an OracleChain after EVERY launch, until every checked
     replica's simulated clock has passed t_target_s and its episode index reached min_episode.
 
     policy: ("table", uint8 [N, N] numpy) or ("mlp", packed fp32 numpy). The log is copied out per
-    launch, so log_capacity only has to hold one launch's records. Returns a summary dict."""
+    launch, so log_capacity only has to hold one launch's records -- unless log_tail: then a launch
+    may write more records than the log ring holds (the bench's own shape: 32 768 hops per launch,
+    8 192 records), and the last log_capacity records of each launch are compared (the earlier
+    ones were overwritten on the device; the counters still cover the whole launch). Returns a
+    summary dict."""
     import torch
     R = eng.R
     picks = list(range(R)) if replicas is None else list(replicas)
@@ -149,6 +156,7 @@ def compare_steady(oracle_mod, eng, topo, params, policy, *, t_target_s, hops_pe
     prev_hops = np.zeros(R, dtype=np.uint64)
     n_cmp = 0
     short = 0                                  # (launch, replica) pairs that executed fewer hops than asked
+    tail_launches = 0                          # (launch, replica) pairs compared on the log's tail only
     ties = [0, 0, 0.0, 0.0]
     max_clock = 0
     for launch in range(max_launches):
@@ -169,13 +177,17 @@ def compare_steady(oracle_mod, eng, topo, params, policy, *, t_target_s, hops_pe
             ch.sync_episode(int(c["episode"]))
             total = int(c["dec_count"])
             new = total - checked[r]
-            assert new <= eng.log_capacity, (label, "a launch wrote more records than the log holds")
-            ref = ch.records(checked[r], new)
+            first = checked[r]
+            if new > eng.log_capacity:
+                assert log_tail, (label, "a launch wrote more records than the log holds")
+                first, new = total - eng.log_capacity, eng.log_capacity
+                tail_launches += 1
+            ref = ch.records(first, new)
             assert len(ref) == new, (label, r, len(ref), new)
-            got_rec = eng.records(r, checked[r], new, log_host=log)
+            got_rec = eng.records(r, first, new, log_host=log)
             if got_rec.tobytes() != ref.tobytes():
                 bad = next(i for i in range(new) if got_rec[i].tobytes() != ref[i].tobytes())
-                raise AssertionError(f"{label} replica {r} launch {launch}: record {checked[r] + bad} differs "
+                raise AssertionError(f"{label} replica {r} launch {launch}: record {first + bad} differs "
                                      f"(t = {int(ref[bad]['t_ns']) / 1e9:.6f} s)\n engine {got_rec[bad]}\n "
                                      f"oracle {ref[bad]}")
             if kind == "mlp" and net_cpu is not None:
@@ -191,6 +203,8 @@ def compare_steady(oracle_mod, eng, topo, params, policy, *, t_target_s, hops_pe
             assert int(c["events_total"]) == ch.events_done + int(ch.o.counters()["events"])
             ch.drop_finished(checked[r])
             max_clock = max(max_clock, int(c["now_ns"]))
+        print(f"  [{label}] launch {launch}: t = {min(chains[r].t_done + int(cnt[r]['now_ns']) for r in picks) / 1e9:.2f} s,"
+              f" {n_cmp} records compared", flush=True)
         done = all(int(cnt[r]["episode"]) >= min_episode and
                    chains[r].t_done + int(cnt[r]["now_ns"]) >= int(t_target_s * 1e9) for r in picks)
         if done:
@@ -200,7 +214,10 @@ def compare_steady(oracle_mod, eng, topo, params, policy, *, t_target_s, hops_pe
     t_min = min(chains[r].t_done + int(cnt[r]["now_ns"]) for r in picks) / 1e9
     out = dict(label=label, launches=launch + 1, records=n_cmp, t_compared_s=t_min,
                episodes=[int(cnt[r]["episode"]) for r in picks], max_clock_s=max_clock / 1e9,
-               hops=int(sum(int(cnt[r]["hops_total"]) for r in picks)), short_launches=short)
+               hops=int(sum(int(cnt[r]["hops_total"]) for r in picks)), short_launches=short,
+               tail_launches=tail_launches, end_diag=[d for r in picks for d in chains[r].end_diag],
+               relay_drops=sum(sum(d["relay_drops"] for d in chains[r].end_diag) + chains[r].o.diag()["relay_drops"]
+                               for r in picks))
     if kind == "mlp" and net_cpu is not None:
         out.update(mlp_decisions=ties[0], torch_disagreements=ties[1], max_abs_dq=ties[2], max_tie_gap=ties[3])
     print(f"\n[steady] {label}: compared up to t = {t_min:.3f} s of simulated time per replica "

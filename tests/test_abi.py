@@ -32,7 +32,7 @@ def test_library_loads_and_exports_every_symbol():
     lib = engine.load_library()
     for name in declared_functions():
         assert hasattr(lib, name), name
-    assert lib.prisma_abi_version() == engine.ABI_VERSION == 9
+    assert lib.prisma_abi_version() == engine.ABI_VERSION == 10
     out = subprocess.run(["nm", "-D", "--defined-only", engine.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (prisma_\w+)", out))
     assert set(declared_functions()) <= exported
@@ -80,6 +80,8 @@ int main(void) {
   printf("%zu %zu %zu %zu\n", offsetof(prisma_params_t, signaling_type), offsetof(prisma_params_t, big_signaling),
          offsetof(prisma_params_t, sync_step_s), offsetof(prisma_params_t, big_signaling_bytes));
   printf("%zu %zu\n", offsetof(prisma_params_t, rng_mode), offsetof(prisma_params_t, rng_stream_offset));
+  printf("%zu %zu %zu\n", sizeof(prisma_kernel_info_t), offsetof(prisma_kernel_info_t, relay_ip),
+         offsetof(prisma_kernel_info_t, relay_dec_bits));
   return 0;
 }
 '''
@@ -107,6 +109,9 @@ def test_ctypes_layouts_match_header():
                    ("signaling_type", "big_signaling", "sync_step_s", "big_signaling_bytes")]
     rng = list(map(int, lines[4].split()))
     assert rng == [engine._Params.rng_mode.offset, engine._Params.rng_stream_offset.offset]
+    ki = list(map(int, lines[5].split()))
+    assert ki == [C.sizeof(engine._KernelInfo), engine._KernelInfo.relay_ip.offset,
+                  engine._KernelInfo.relay_dec_bits.offset]
 
 
 def test_engine_refuses_without_gpu():

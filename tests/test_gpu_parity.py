@@ -418,15 +418,30 @@ def test_tunnel_ttl_expiry_parity(oracle_mod):
     run_table_both(oracle_mod, topo, params, 3, 10 ** 6, table)
 
 
-def test_tunnel_big_log_parity(oracle_mod):
-    """A log beyond 2^18 decisions on a tunnelled overlay runs the kernels whose relay entries keep
-    the 22-bit decision index (engine_layout.h rip_make; the host's instance pick)."""
+@pytest.mark.parametrize("log_bits,relay_ip", [(17, 1), (18, 0), (19, 0)])
+def test_tunnel_log_capacity_kernel_pick(log_bits, relay_ip):
+    """The library's own report of the instance prisma_create picked (prisma_kernel_info): the
+    relay-entry kernels keep 18 bits of the decision index (engine_layout.h rip_make), so their
+    log-wrap check holds only for logs below 2^18; a log of 2^18 or more takes the 22-bit kernels."""
     topo = Topology.example("overlay_full_mesh_3n_abilene", 0, 20.0)
-    params = engine_params(topo, sim_time_s=10.0, ping_as_obs=0, seed=7, log_capacity=1 << 19)
+    params = engine_params(topo, sim_time_s=10.0, ping_as_obs=0, seed=7, log_capacity=1 << log_bits)
     eng = PrismaEngine(topo, params, 1)
-    assert eng.kernel_name.endswith("true, true>")            # TUN, CTRL instance
+    ki = eng.kernel_info()
     eng.close()
-    cnt = run_table_both(oracle_mod, topo, params, 2, 3000, _random_table(topo, 7))
+    assert ki["tunnels"] == 1 and ki["relay_ip"] == relay_ip and ki["ctrl"] == 1 - relay_ip
+    assert ki["relay_dec_bits"] == (18 if relay_ip else 22)
+    assert (1 << log_bits) < (1 << ki["relay_dec_bits"])       # every log age is representable
+    assert eng.kernel_name.endswith("true, false>" if relay_ip else "true, true>")
+
+
+def test_tunnel_big_log_parity(oracle_mod):
+    """A log of 2^19 decisions on a tunnelled overlay (the 22-bit relay-entry kernels) run past
+    2^18 decisions: 300 000 hops on one replica of the 3-node mesh at load factor 20 in a 150-s
+    episode, every record in the log compared, so relay entries carry decision indices above 2^18."""
+    topo = Topology.example("overlay_full_mesh_3n_abilene", 0, 20.0)
+    params = engine_params(topo, sim_time_s=150.0, ping_as_obs=0, seed=7, log_capacity=1 << 19)
+    cnt = run_table_both(oracle_mod, topo, params, 1, 300000, _random_table(topo, 7))
+    assert int(cnt["dec_count"][0]) > (1 << 18)
     assert cnt["ov_lost"].sum() > 0
 
 

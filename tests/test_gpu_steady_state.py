@@ -51,6 +51,83 @@ def test_config2_headline_full_episode_and_auto_reset(oracle_mod):
     assert out["short_launches"] == 0
 
 
+def test_config2_headline_at_bench_shape(oracle_mod):
+    """The headline at the bench's own launch shape (bench.py PRESETS["config2"] and measure()):
+    32 768 hops per replica per launch into a log ring of 8 192 records, auto-reset, seed 100.
+    A launch writes ~4x the records the ring holds, so the ring wraps inside every launch: the
+    last 8 192 records of each launch and every counter are compared, through the 60-s episode
+    end (about every 4 launches at this shape) and the spare-image restart into episode 1, on
+    two of the bench's replicas (global ids 4094, 4095)."""
+    from prisma_amd.policies import StackedQNet
+    topo = Topology.example("abilene", 0, 1.0)
+    table = StackedQNet(topo, "routing", seed=1234, device="cpu").argmin_table().numpy()
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=1, auto_reset=1, seed=100, replica_base=4094,
+                           log_capacity=8192)
+    eng = PrismaEngine(topo, params, 2)
+    assert eng.log_capacity == 8192
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("table", table), t_target_s=65.0,
+                         hops_per_launch=32768, min_episode=1, log_tail=True,
+                         label="config 2 abilene dq_routing, bench shape (32768 hops, log 8192)")
+    eng.close()
+    assert out["t_compared_s"] >= 65.0 and min(out["episodes"]) >= 1
+    assert out["short_launches"] == 0
+    assert out["tail_launches"] == 2 * out["launches"]         # the ring wrapped inside every launch
+
+
+def test_config3_abilene_on_geant_dqn_buffer_episode_end(oracle_mod):
+    """Config 3 through the regime its bench runs in: the tunnelled-overlay kernels (relay entries
+    with the tunnel target, LDS FIFO windows, engine_core.h q_put / q_take) from t = 0 past the 60-s
+    episode end (Simulator::Stop, /root/reference/prisma/ns3/sim.cc:703-716; main.py:111-115's
+    episode loop) and the spare-image restart (engine_core.h spare_restart) into episode 1,
+    DQN-buffer with pingAsObs=1, near-ties checked against torch fp32, on 2 replicas."""
+    topo = Topology.example("abilene_on_geant", 0, 1.0)
+    net, w = _buffer_net(topo, seed=7)
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=1, auto_reset=1, seed=100, replica_base=4001,
+                           log_capacity=65536)
+    eng = PrismaEngine(topo, params, 2)
+    assert eng.kernel_info()["relay_ip"] == 1                  # the benchmarked (relay-entry) kernels
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("mlp", w), t_target_s=65.0, hops_per_launch=16384,
+                         min_episode=1, net_cpu=net, label="config 3 abilene-on-geant dqn_buffer 60-s episode end")
+    eng.close()
+    assert out["t_compared_s"] >= 65.0 and min(out["episodes"]) >= 1
+    assert out["short_launches"] == 0
+
+
+def _random_table(topo, seed):
+    rng = np.random.default_rng(seed)
+    table = np.zeros((topo.n_nodes, topo.n_nodes), dtype=np.uint8)
+    for u in topo.overlay_nodes:
+        table[u] = rng.integers(0, topo.degrees[u], topo.n_nodes)
+    return table
+
+
+@pytest.mark.parametrize("ping", [0, 1])
+def test_tunnel_table_short_episodes_deep_fifos(oracle_mod, ping):
+    """Table-policy twin of the config-3 episode-end test on the shipped 3-node tunnelled mesh at
+    load factor 20: 4-s episodes, auto-reset, a random action table. FIFOs inside tunnels overflow
+    (drops charged to the sender, data-packet-manager.cc:88-106; ipv4-interface.cc:213-229) and
+    every episode ends with FIFOs deeper than the LDS window, so packets sit in both the LDS
+    windows and the HBM ring when the spare image replaces the state. Compared through 3 episode
+    ends."""
+    topo = Topology.example("overlay_full_mesh_3n_abilene", 0, 20.0)
+    table = _random_table(topo, 11 + ping)
+    params = engine_params(topo, sim_time_s=4.0, ping_as_obs=ping, auto_reset=1, seed=23, replica_base=70 + ping,
+                           log_capacity=65536)
+    eng = PrismaEngine(topo, params, 2)
+    assert eng.kernel_info()["relay_ip"] == 1
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("table", table), t_target_s=13.0, hops_per_launch=8192,
+                         min_episode=3, label=f"3-node tunnelled mesh lf 20 pingAsObs {ping}, 4-s episodes")
+    eng.close()
+    assert out["t_compared_s"] >= 13.0 and min(out["episodes"]) >= 3
+    assert out["relay_drops"] > 0                              # drops on FIFOs inside tunnels
+    ends = out["end_diag"]
+    assert len(ends) >= 6 and all(d["deep_fifos"] > 0 for d in ends), ends   # LDS window + HBM ring in use
+    print(f"[steady] episode ends: {ends}; drops inside tunnels: {out['relay_drops']}")
+
+
 @pytest.mark.parametrize("ping", [0, 1])
 @pytest.mark.parametrize("lf", [0.5, 1.0, 2.0])
 def test_config4_geant_dqn_buffer_steady(oracle_mod, lf, ping):
