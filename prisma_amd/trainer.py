@@ -262,7 +262,7 @@ class QRoutingTrainer:
                  big_signaling_size: int = 512, packet_size: int = 512, pending_cap: int = 1 << 20,
                  n_replicas: int = 1, signaling_sim: int = 1, sync_step: float = 1.0, sync_ratio: float = 0.1,
                  link_cap: int = 500000, link_delay_ms: float = 1.0, prioritized_replay: bool = False,
-                 max_snapshots: Optional[int] = None):
+                 max_snapshots: Optional[int] = None, warn_stored_bytes: Optional[int] = 1 << 30):
         if signaling_type not in ("ideal", "NN", "target"):
             raise ValueError("signaling_type must be 'ideal', 'NN' or 'target'")
         self.topo = topo
@@ -338,6 +338,12 @@ class QRoutingTrainer:
         self.max_snapshots = None if max_snapshots is None else int(max_snapshots)
         self.stale_syncs = 0                         # syncs that received an older stored generation
         self._stale_warned = False
+        # what the stored generations cost: their bytes, the peak count and bytes (stats()), and a
+        # one-time warning past warn_stored_bytes (None: never) -- a report, the semantics unchanged
+        self.generation_bytes = sum(t.numel() * t.element_size() for t in self.q.state_dict().values())
+        self.warn_stored_bytes = None if warn_stored_bytes is None else int(warn_stored_bytes)
+        self.peak_generations = 0
+        self._bytes_warned = False
         self._gen_w = {}                             # generation key -> stacked weights
         self._snap_gen = {}                          # version -> generation key
         self.version = 0
@@ -740,14 +746,27 @@ class QRoutingTrainer:
                     self._stale_warned = True
                 return self._snap_gen[max(self._snap_gen)]
             self._gen_w[key] = self._snapshot()
+            n = len(self._gen_w)
+            self.peak_generations = max(self.peak_generations, n)
+            if (self.warn_stored_bytes is not None and not self._bytes_warned
+                    and n * self.generation_bytes > self.warn_stored_bytes):
+                warnings.warn(f"QRoutingTrainer: {n} stored weight generations hold {n * self.generation_bytes} bytes "
+                              f"(> warn_stored_bytes={self.warn_stored_bytes}); replica clocks far apart keep old "
+                              "copies alive. A smaller sync_step or train_every, or max_snapshots, bounds them",
+                              RuntimeWarning, stacklevel=3)
+                self._bytes_warned = True
         return key
 
     def stats(self) -> dict:
         """The trainer's own counters (not the reference's Agent statistics): signalling overheads,
-        stored weight generations and the syncs that received an older generation (max_snapshots)."""
+        stored weight generations (now and at their peak, count and bytes) and the syncs that received
+        an older generation (max_snapshots)."""
         return {"small_signaling_bytes": float(self.small_overhead), "small_signaling_pkts": int(self.small_pkts),
                 "big_signaling_bits": float(self.big_overhead), "big_signaling_pkts": int(self.big_pkts),
-                "stored_generations": len(self._gen_w), "stale_syncs": int(self.stale_syncs)}
+                "stored_generations": len(self._gen_w), "stale_syncs": int(self.stale_syncs),
+                "stored_bytes": len(self._gen_w) * self.generation_bytes,
+                "peak_generations": int(self.peak_generations),
+                "peak_stored_bytes": int(self.peak_generations) * self.generation_bytes}
 
     def weights_of(self, version: int) -> dict:
         """The stacked online weights copy `version` refers to."""

@@ -619,6 +619,72 @@ def test_syncs_copy_the_current_weights_without_a_cap():
     assert syncs > 32 and tr.stale_syncs == 0 and tr.stats()["stale_syncs"] == 0
 
 
+def test_stored_bytes_warning_keeps_the_semantics():
+    """warn_stored_bytes only reports: past the threshold one RuntimeWarning names the bytes, and
+    every sync still copies the current weights (the default, uncapped semantics); stats() carries
+    the stored and peak generation counts and bytes."""
+    topo = Topology.example("abilene")
+    R = 64
+    tr = QRoutingTrainer(topo, "buffer", seed=4, device="cpu", n_replicas=R, sync_step=0.01, batch_size=4)
+    gb = tr.generation_bytes
+    assert gb == sum(t.numel() * t.element_size() for t in tr.q.state_dict().values()) > 0
+    tr.warn_stored_bytes = 3 * gb
+    rng = np.random.default_rng(7)
+    clock = np.zeros(R)
+    speed = rng.random(R) * 0.004
+    g = torch.Generator().manual_seed(2)
+    import warnings as _w
+    with _w.catch_warnings(record=True) as caught:
+        _w.simplefilter("always")
+        for step in range(40):
+            clock += speed
+            tr.advance_clock(torch.from_numpy((clock * 1e9).astype(np.int64)))
+            v0 = tr.version
+            tr.check_sync()
+            if tr.version != v0:
+                cur = tr.q.state_dict()
+                for k, t in tr.weights_of(tr.version).items():
+                    assert torch.equal(t, cur[k]), (step, k)
+            with torch.no_grad():
+                for p in tr.q.parameters():
+                    p.add_(1e-3 * torch.randn(p.shape, generator=g))
+    msgs = [str(w.message) for w in caught if "warn_stored_bytes" in str(w.message)]
+    assert len(msgs) == 1, msgs
+    st = tr.stats()
+    assert st["peak_generations"] > 3 and st["peak_stored_bytes"] == st["peak_generations"] * gb
+    assert st["stored_bytes"] == st["stored_generations"] * gb <= st["peak_stored_bytes"]
+    assert tr.stale_syncs == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not torch.cuda.is_available(), reason="needs an MI355X")
+def test_stored_generations_at_4096_abilene_replicas():
+    """The trainer's stored weight generations in a training run at the headline's replica count
+    (4 096 Abilene replicas, the engine in external-action mode, an optimizer step every 4 env
+    steps, syncs every 20 ms of each replica's simulated clock, "ideal" signalling; the default
+    uncapped semantics). A copy lives until its (replica, node) syncs twice more, so the generations
+    alive at once span about two sync periods of the slowest replica, not the replica count: the
+    peak is bounded by the optimizer steps of that window. Stated bound for this run: 64
+    generations (the run makes 150 optimizer steps)."""
+    from prisma_amd.env import VecRoutingEnv
+    from prisma_amd.trainer import train
+    R, steps, every = 4096, 600, 4
+    env = VecRoutingEnv("abilene", n_replicas=R, sim_time_s=60.0, ping_as_obs=0)
+    tr = QRoutingTrainer(env.topo, "buffer", batch_size=512, buffer_size=50000, seed=0, n_replicas=R,
+                         sync_step=0.02)
+    losses = train(env, tr, steps=steps, train_every=every)
+    env.close()
+    st = tr.stats()
+    print(f"\n[trainer] R={R}: {steps} env steps, {int(tr.steps.max())} optimizer steps, sim clock "
+          f"{tr.clock.min():.3f}-{tr.clock.max():.3f} s, syncs (versions) {tr.version}, stored generations "
+          f"{st['stored_generations']} ({st['stored_bytes']} B), peak {st['peak_generations']} "
+          f"({st['peak_stored_bytes']} B, {tr.generation_bytes} B each)")
+    assert losses and np.all(np.isfinite(losses))
+    assert tr.version > 20                                   # many syncs happened
+    assert st["peak_generations"] <= 64 and st["peak_stored_bytes"] == st["peak_generations"] * tr.generation_bytes
+    assert st["stale_syncs"] == 0
+
+
 def test_trainer_stats_tblog(tmp_path):
     from prisma_amd import tblog
     topo = Topology.example("abilene")
