@@ -196,6 +196,10 @@ struct Regs {
     static constexpr int NF = 4, NL = 16;
     static constexpr bool kLazy = true;          // empty-queue transmit completions elided (lazy_resolve)
     static constexpr bool kMem = false;
+    // the draw cache's code (flow_next) in the instances of up to 128 flows: larger scenarios
+    // have no LDS room for it (GEANT's 506 flows: 4 KB at 8 replicas per CU), and its code cost
+    // their register allocation 1.3 % (config 4)
+    static constexpr bool kDcache = FS <= 2;
     // not staged: each lane's earliest flow (time, seq, code), refreshed when one of its flows
     // changes (flow_set, ~0.3 per hop) instead of on every event selection (~2.6 per hop)
     int64_t fm_t;
@@ -260,7 +264,7 @@ struct LV {
     __device__ __forceinline__ uint32_t topo_bytes() const { return (uint32_t)u(offsetof(Layout, topo_bytes) / 4); }
     __device__ __forceinline__ uint32_t state_bytes() const { return (uint32_t)u(offsetof(Layout, state_bytes) / 4); }
     __device__ __forceinline__ uint32_t lds_bytes() const { return (uint32_t)u(offsetof(Layout, lds_bytes) / 4); }
-    __device__ __forceinline__ uint32_t table_bytes() const { return (uint32_t)u(offsetof(Layout, table_bytes) / 4); }
+    __device__ __forceinline__ uint32_t s_dcache() const { return (uint32_t)u(offsetof(Layout, s_dcache) / 4); }
     __device__ __forceinline__ uint32_t s_hdr() const { return (uint32_t)u(offsetof(Layout, s_hdr) / 4); }
     __device__ __forceinline__ uint32_t s_cnt() const { return (uint32_t)u(offsetof(Layout, s_cnt) / 4); }
     __device__ __forceinline__ uint32_t s_obs() const { return (uint32_t)u(offsetof(Layout, s_obs) / 4); }
@@ -1242,18 +1246,52 @@ __device__ __forceinline__ void flow_next(const Sim& S, RS& R, Hot& H, uint32_t 
         flow_set(S, R, H, f, H.now + sec_to_ns(delay), H.seq++, draw + 1);
         return;
     }
+    // The draw cache (register-resident engine, where LDS has room: Layout::s_dcache = LDS offset
+    // | K): a flow's draws come in groups of K (2 or 3). The first draw of a group is computed in
+    // lane 0 and the next K - 1 in lanes 1 .. K-1 by the same vector instructions -- Philox, the
+    // logarithm and the conversion cost one draw -- and their send delays wait in the flow's LDS
+    // slots for its next sends. Every draw keeps its own Philox counter (flow, draw, episode), so
+    // the values are the uncached ones; an episode starts each flow at draw 0, which refills the
+    // slots before the first read.
+    constexpr bool kDc = !RS::kMem && RS::kDcache;
+    const uint32_t dcw = kDc ? S.lv.s_dcache() : 0u;
+    if (kDc && dcw != 0u) {
+        const uint32_t K = dcw & 15u;
+        int64_t* slot = (int64_t*)(S.base + (dcw & ~15u)) + f * (K - 1u);
+        const uint32_t g = (K == 2u) ? (draw & 1u) : draw - 3u * (uint32_t)(((uint64_t)draw * 0xAAAAAAABull) >> 33);
+        int64_t dns;
+        if (g != 0u) {
+            dns = u_ld64(slot + (g - 1u));
+        } else {
+            const uint32_t j = (uint32_t)S.lane < K ? (uint32_t)S.lane : 0u;
+            uint32_t c[4] = { f, draw + j, H.episode, 1u };
+            philox4x32_10(c, S.lv.seed_lo(), S.gid);
+            const uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
+            const double U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
+            const int64_t dn = sec_to_ns(-t_fmean(S, f) * det_log(U));
+            if (j != 0u) slot[j - 1u] = dn;
+            dns = mk64(rfl(lo32(dn)), rfl(hi32(dn)));
+        }
+        flow_set(S, R, H, f, H.now + dns, H.seq++, draw + 1);
+        return;
+    }
     uint32_t c[4] = { f, draw, H.episode, 1u };                   // poisson-application.cc:265-295
     // The table-policy instances run the rounds on the vector unit (the values pass through
     // VGPRs, so the compiler cannot keep them scalar) and take back the two words they use:
     // ~80 scalar instructions per flow event moved off the headline's busiest unit.  The MLP
     // instances keep the scalar rounds with their keys hoisted out of the event loop.
     uint32_t k0 = S.lv.seed_lo(), k1 = S.gid;
+    if (PRISMA_ABLATE & 8) {                                      // diagnostic: a cheap hash, not Philox
+        c[0] = (f * 2654435761u) ^ (draw * 2246822519u) ^ (k1 * 3266489917u) ^ H.episode;
+        c[1] = c[0] * 668265263u ^ (c[0] >> 15);
+    } else {
     if (!S.mlp_inst) asm volatile("" : "+v"(c[0]), "+v"(c[1]), "+v"(c[2]), "+v"(c[3]), "+v"(k0), "+v"(k1));
     philox4x32_10(c, k0, k1);
     if (!S.mlp_inst) { c[0] = __builtin_amdgcn_readfirstlane(c[0]); c[1] = __builtin_amdgcn_readfirstlane(c[1]); }
+    }
     uint64_t u53 = ((uint64_t)(c[0] >> 5) << 26) | (uint64_t)(c[1] >> 6);
     double U = ((double)u53 + 1.0) * (1.0 / 9007199254740992.0);
-    double delay = -t_fmean(S, f) * det_log(U);
+    double delay = (PRISMA_ABLATE & 16) ? -t_fmean(S, f) * (double)__logf((float)U) : -t_fmean(S, f) * det_log(U);
     int64_t t = H.now + sec_to_ns(delay);
     if constexpr (RS::kMem) TM_FLOW(2);
     flow_set(S, R, H, f, t, H.seq++, draw + 1);

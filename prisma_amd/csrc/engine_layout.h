@@ -177,7 +177,9 @@ __host__ __device__ inline uint32_t ti_len(uint32_t ti) { return ti >> 24; }
 // from a device copy.
 struct Layout {
     int32_t N, E, L, F, W, max_deg, WCAP, MA;
-    uint32_t topo_bytes, state_bytes, lds_bytes, table_bytes;
+    uint32_t topo_bytes, state_bytes, lds_bytes;
+    uint32_t s_dcache;           // register engine: LDS offset of the flows' cached next-send delays
+                                 // (engine_core.h flow_next), 0 where LDS has no room for them
     // state image (LDS offset 0) and the action table (LDS offset lds_state_bytes)
     uint32_t s_hdr, s_cnt, s_obs, s_wt, s_wseq, s_ring, s_win, s_pbd, s_mlp;
     int32_t  T, NO;              // tunnels, overlay nodes
@@ -220,6 +222,7 @@ struct Layout {
     // image) only where that costs no replica per CU; otherwise it is read from HBM (L2)
     uint32_t table_in_lds;
     uint32_t lds_mlp_bytes;      // LDS of a DQN-buffer launch (its 256 B of activations included)
+    uint32_t table_bytes;        // the [N][N] action table
 };
 constexpr uint32_t kLVWords = 64u;           // Layout dwords held in the LV register
 

@@ -285,6 +285,10 @@ PRISMA_TU_TIMING(prisma_debug_timing)
 extern "C" const char* prisma_last_error(void) { return g_err.c_str(); }
 
 static uint32_t align16(uint32_t x) { return (x + 15u) & ~15u; }
+// largest draw-cache group (build_layout; 2 or 3, engine_core.h flow_next; 1: no cache)
+#ifndef PRISMA_DCACHE_KMAX
+#define PRISMA_DCACHE_KMAX 3u
+#endif
 static uint32_t next_pow2(uint32_t x) { uint32_t p = 1; while (p < x) p <<= 1; return p; }
 
 // Overlay of a topology (host): tunnels, routing, control-packet load per link.
@@ -915,20 +919,32 @@ static int build_layout(const prisma_topology_t* T, const prisma_params_t* P, La
     L.s_win = take(4u * (uint32_t)OP.T * L.MA);
     L.s_pbd = take(4u * (uint32_t)(OP.tunnels ? OP.n_resp : OP.T) * L.PBK);
     if (L.rng_mode) take(kRngBytes);                // ns-3 streams: the last kRngBytes (engine_core.h)
-    L.lds_state_bytes = o;
-    if (OP.tunnels) L.s_ring = take(4u * tot);      // HBM part of the image
-    L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 16u * 64u * (uint32_t)ls));
-    L.state_bytes = o;
     // Replicas per CU are bounded by LDS (160 KiB / bytes per replica) for the larger
     // topologies, and a launch whose replicas do not all fit at once runs in rounds
     // (GEANT + MLP: 2 048 replicas at 7 per CU took two rounds, the second 1/8 full).
-    // So the action table goes to LDS only where it costs no replica per CU (else the
-    // decision reads it from HBM, L2-resident), and the DQN-buffer activations reuse the
-    // table's LDS, dead in MLP launches, when it is there.
     const uint32_t tb = align16(L.table_bytes);
     // (waves per CU of the step kernel: StepOcc, 4 SIMDs x its waves per SIMD)
     const uint32_t occ = 4u * ((fs <= 2 && ls == 1) ? 4u : (ls <= 2 ? 2u : 1u));
     auto per_cu = [occ](uint32_t b) { const uint32_t n = (160u * 1024u) / (b ? b : 1u); return n < occ ? n : occ; };
+    // The flows' draw cache (engine_core.h flow_next: K - 1 next-send delays of 8 B per flow,
+    // computed in lanes 1 .. K-1 with the draw before them; K = 3, else 2) where it costs no
+    // replica per CU, the action table's LDS placement counted as it would be without it; not
+    // with ns-3 streams. Layout::s_dcache = its 16-B aligned offset | K.
+    L.s_dcache = 0u;
+    if (!L.rng_mode && F > 0 && fs <= 2) {         // (the instances with its code: Regs::kDcache)
+        const uint32_t t0 = per_cu(o + tb) == per_cu(o) ? tb : 0u;
+        for (uint32_t K = PRISMA_DCACHE_KMAX; K >= 2u; --K) {
+            const uint32_t dc = align16(8u * (K - 1u) * (uint32_t)F);
+            if (per_cu(o + dc + t0) == per_cu(o + t0)) { L.s_dcache = take(dc) | K; break; }
+        }
+    }
+    L.lds_state_bytes = o;
+    if (OP.tunnels) L.s_ring = take(4u * tot);      // HBM part of the image
+    L.s_regs = take(4u * (4u * 64u * (uint32_t)fs + 16u * 64u * (uint32_t)ls));
+    L.state_bytes = o;
+    // The action table goes to LDS only where it costs no replica per CU (else the decision
+    // reads it from HBM, L2-resident), and the DQN-buffer activations reuse the table's LDS,
+    // dead in MLP launches, when it is there.
     L.table_in_lds = per_cu(L.lds_state_bytes + tb) == per_cu(L.lds_state_bytes) ? 1u : 0u;
     L.lds_bytes = L.lds_state_bytes + (L.table_in_lds ? tb : 0u);
     L.s_mlp = (L.table_in_lds && tb >= 256u) ? L.lds_state_bytes : L.lds_bytes;

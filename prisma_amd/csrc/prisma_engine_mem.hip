@@ -27,6 +27,7 @@
 struct MemSt {
     static constexpr bool kLazy = true;          // empty-queue transmit completions elided (lazy_resolve)
     static constexpr bool kMem = true;
+    static constexpr bool kDcache = false;       // (no draw cache: engine_core.h flow_next)
     uint32_t* lrec;              // [L][RW] link records (HBM)
     uint4* fkeys;                // [FG] flow leaf keys {t lo, t hi, seq, draw} (HBM)
     uint2* lkey;                 // LDS [L] link leaf keys {t lo, seq}: t = now + (t lo - lo32(now))
