@@ -26,7 +26,9 @@ using namespace prisma;
 
 // Diagnostic timing builds only (scripts/ablate.sh; results are NOT the
 // reference's): bit 0 skips the previous-record read (relay entries carry
-// dst/start), bit 1 skips the decision-record stores, bit 2 skips observe().
+// dst/start), bit 1 skips the decision-record stores, bit 2 skips observe(), bit 3 draws from a
+// cheap hash instead of Philox, bit 4 takes a float log, bit 5 drops the reward's microsecond
+// formatting, bit 6 replaces the ping statistic by queued bytes (profiles/r06_ab/).
 #ifndef PRISMA_ABLATE
 #define PRISMA_ABLATE 0
 #endif
@@ -940,7 +942,7 @@ __device__ __forceinline__ uint32_t observe_links(const Sim& S, const Regs<FS, L
 #pragma unroll
     for (int j = 0; j < LS; ++j) {
         uint32_t val;
-        if (pobs)
+        if (pobs && !(PRISMA_ABLATE & 64))
             val = ping_value_lane(ld_d(R.pav_lo.v[j], R.pav_hi.v[j]), R.pm_lo.v[j], ld_d(R.od_lo.v[j], R.od_hi.v[j]),
                                   H.ping_rounds, now_s);
         else
@@ -2100,7 +2102,8 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
             dst = (w_prev >> 8) & 255u;
             start = w_prev >> 16;
             last = w_prev & 255u;
-            reward = us_to_sec(py_micros(H.now)) - us_to_sec(py_micros(t_prev));   // forwarder.py:360
+            reward = (PRISMA_ABLATE & 32) ? (double)(uint32_t)(H.now - t_prev)        // (diagnostic builds only)
+                                          : us_to_sec(py_micros(H.now)) - us_to_sec(py_micros(t_prev));   // forwarder.py:360
             CNT_ADD(S, reward_sum, reward);
         }
         // obs[0] = m_map_overlay_array[dst] (the identity on identity overlays)
