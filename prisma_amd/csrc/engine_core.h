@@ -32,6 +32,9 @@ using namespace prisma;
 #ifndef PRISMA_ABLATE
 #define PRISMA_ABLATE 0
 #endif
+#ifndef PRISMA_REWARD_LANES
+#define PRISMA_REWARD_LANES 1
+#endif
 
 
 // instruction-count experiments (A/B builds)
@@ -594,6 +597,8 @@ __device__ __forceinline__ void link_put(const Sim& S, Regs<FS, LS>& R, const Ho
 
 __device__ __forceinline__ int64_t wave_min_i64(int64_t v);
 __device__ __forceinline__ uint32_t wave_umin_fast(uint32_t v);
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v);
 
 // Elided completions.  A transmit completion that finds its queue empty only clears
 // `busy` (point-to-point-net-device.cc:305-336: TransmitComplete with no packet left
@@ -2102,8 +2107,23 @@ __device__ __forceinline__ int on_arrive(const Sim& S, RS& R, Hot& H, uint32_t l
             dst = (w_prev >> 8) & 255u;
             start = w_prev >> 16;
             last = w_prev & 255u;
-            reward = (PRISMA_ABLATE & 32) ? (double)(uint32_t)(H.now - t_prev)        // (diagnostic builds only)
-                                          : us_to_sec(py_micros(H.now)) - us_to_sec(py_micros(t_prev));   // forwarder.py:360
+            if (PRISMA_ABLATE & 32) {
+                reward = (double)(uint32_t)(H.now - t_prev);                  // (diagnostic builds only)
+            } else if (PRISMA_REWARD_LANES) {
+                // the reward's two clock terms (forwarder.py:360) in lanes 0 and 1 of one vector
+                // evaluation -- now in even lanes, the previous decision's time in odd ones -- and
+                // lane 0 takes the difference with lane 1's term brought over by a DPP move
+                const uint32_t m = S.m1;                                      // -(lane & 1)
+                const int64_t tt = mk64((lo32(t_prev) & m) | (lo32(H.now) & ~m), (hi32(t_prev) & m) | (hi32(H.now) & ~m));
+                const double us = us_to_sec(py_micros(tt));
+                const uint64_t ub = (uint64_t)__double_as_longlong(us);
+                const double up = __longlong_as_double((long long)mk64(dpp_u32<0xB1, 0xF>((uint32_t)ub),
+                                                                       dpp_u32<0xB1, 0xF>((uint32_t)(ub >> 32))));
+                const uint64_t rb = (uint64_t)__double_as_longlong(us - up);
+                reward = __longlong_as_double((long long)mk64(rfl((uint32_t)rb), rfl((uint32_t)(rb >> 32))));
+            } else {
+                reward = us_to_sec(py_micros(H.now)) - us_to_sec(py_micros(t_prev));   // forwarder.py:360
+            }
             CNT_ADD(S, reward_sum, reward);
         }
         // obs[0] = m_map_overlay_array[dst] (the identity on identity overlays)
