@@ -42,3 +42,25 @@ def test_cpu_baseline_table_and_mlp(oracle_mod):
     r = bench.cpu_baseline(topo, params, "mlp", w, 5000, 2000, threads=2, warm_hops=500, workload="abilene mlp")
     assert r["cores"] <= 2 and r["value"] > 0 and "DQN-buffer MLP" in r["sample"] and "500 hops untimed" in r["sample"]
     assert r["workload"] == "abilene mlp"
+
+
+def test_cpu_baseline_worker_failure_ends_promptly(oracle_mod, monkeypatch):
+    """A worker that raises (here: its oracle cannot be built) aborts the threads' barrier, so
+    cpu_baseline raises at once instead of waiting for the rank deadline."""
+    import time
+    topo = Topology.example("abilene")
+    params = engine_params(topo, sim_time_s=2.0, ping_as_obs=1, auto_reset=0, seed=100)
+
+    class Broken:
+        def __init__(self, *a, **k):
+            raise MemoryError("no oracle")
+
+    monkeypatch.setattr(oracle_mod, "OracleSim", Broken)
+    t0 = time.perf_counter()
+    try:
+        bench.cpu_baseline(topo, params, "table", sp_next_hop_table(topo), 1000, 1000, threads=2)
+    except RuntimeError as e:
+        assert "cpu_baseline worker failed" in str(e)
+    else:
+        raise AssertionError("cpu_baseline returned with a failing worker")
+    assert time.perf_counter() - t0 < 30.0

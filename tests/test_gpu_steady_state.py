@@ -144,6 +144,24 @@ def test_config4_geant_dqn_buffer_steady(oracle_mod, lf, ping):
     assert out["t_compared_s"] >= 15.0 and out["mlp_decisions"] > 10000
 
 
+def test_config4_geant_dqn_buffer_episode_ends(oracle_mod):
+    """Config 4's instance (identity overlay, in-kernel DQN-buffer, 8 flow and 2 link slots) through
+    two episode ends inside launches: 6-s episodes, auto-reset, so the spare-image restart and the
+    second event-loop copy (step_kernel.h) run the MLP, compared through t = 13 s."""
+    topo = Topology.example("geant", 0, 1.0)
+    net, w = _buffer_net(topo, seed=43)
+    params = engine_params(topo, sim_time_s=6.0, ping_as_obs=0, auto_reset=1, seed=100, replica_base=1500,
+                           log_capacity=65536)
+    eng = PrismaEngine(topo, params, 2)
+    ki = eng.kernel_info()
+    assert (ki["flow_slots"], ki["link_slots"], ki["tunnels"], ki["ctrl"]) == (8, 2, 0, 0)
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("mlp", w), t_target_s=13.0, hops_per_launch=16384,
+                         min_episode=2, net_cpu=net, label="config 4 geant dqn_buffer 6-s episodes")
+    eng.close()
+    assert out["t_compared_s"] >= 13.0 and min(out["episodes"]) >= 2 and out["short_launches"] == 0
+
+
 def test_config3_abilene_on_geant_dqn_buffer_steady(oracle_mod):
     """Config 3: the Abilene overlay tunnelled over GEANT, DQN-buffer, pingAsObs=1, 15 s."""
     topo = Topology.example("abilene_on_geant", 0, 1.0)
