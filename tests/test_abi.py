@@ -219,3 +219,25 @@ def test_plan_tunnelled_overlay():
     bad.flow_src[0] = 1                                  # underlay-only node 1
     with pytest.raises(engine.PrismaError, match="overlay"):
         engine.plan(bad, engine_params(bad))
+
+
+def test_plan_draw_cache_keeps_replicas_per_cu():
+    """The flows' draw cache (engine_core.h flow_next: K - 1 cached 8-B send delays per flow) is laid
+    out only where it costs no replica per CU (prisma_engine.hip build_layout): K = 3 on Abilene
+    (110 flows: 1 760 B, 16 replicas of 9 728 B per 160-KiB CU as without it) and Abilene-on-GEANT,
+    none on GEANT (506 flows at 8 replicas per CU), none with ns-3 streams (their state ends the
+    image) and none on the memory-resident engine."""
+    from prisma_amd.config import engine_params
+    from prisma_amd.topology import Topology
+    per_cu = lambda b: min(16, (160 * 1024) // b)
+    ab = Topology.example("abilene")
+    p = engine.plan(ab, engine_params(ab))
+    assert p["lds_bytes"] == 7968 + 2 * 8 * 110 and per_cu(p["lds_bytes"]) == per_cu(7968) == 16
+    q = engine.plan(ab, engine_params(ab, rng="ns3"))
+    assert q["lds_state_bytes"] == 7840 + 112                      # no cache; the ns-3 stream state instead
+    m = engine.plan(ab, engine_params(ab, engine=engine.PRISMA_ENGINE_MEMORY))
+    assert m["lds_state_bytes"] == 128 + 160 + 16 + 2 * 16 + 2 * 16 + 320 + 48
+    ge = Topology.example("geant")
+    assert engine.plan(ge, engine_params(ge))["lds_bytes"] == 20400
+    aog = Topology.example("abilene_on_geant")
+    assert engine.plan(aog, engine_params(aog))["lds_bytes"] == 7232 + 2 * 8 * 110
