@@ -75,6 +75,31 @@ def test_config2_headline_at_bench_shape(oracle_mod):
     assert out["tail_launches"] == 2 * out["launches"]         # the ring wrapped inside every launch
 
 
+@pytest.mark.parametrize("preset,t_target,min_ep", [("config3", 65.0, 1), ("config4", 15.0, 0), ("config5", 3.0, 0)])
+def test_dqn_configs_at_bench_shape(oracle_mod, preset, t_target, min_ep):
+    """Configs 3-5 at their bench presets' own launch shape (bench.py PRESETS: hops per replica per
+    launch; measure(): log capacity 8 192, 65 536 beyond 256 links; auto-reset, seed 100, the
+    random-init DQN-buffer weights of seed 1234), with the log tail compared where a launch writes
+    more records than the ring holds. Config 3 runs through its 60-s episode end."""
+    import bench
+    from prisma_amd.policies import StackedQNet
+    pr = bench.PRESETS[preset]
+    topo = Topology.example(pr["topology"], 0, 1.0)
+    net = StackedQNet(topo, "buffer", seed=1234, device="cpu")
+    w = net.pack().numpy()
+    log_cap = 65536 if topo.n_links > 256 else 8192
+    R = 1 if preset == "config5" else 2
+    params = engine_params(topo, sim_time_s=60.0, ping_as_obs=pr["ping_as_obs"], auto_reset=1, seed=100,
+                           replica_base=pr["replicas"] - R, log_capacity=log_cap)
+    eng = PrismaEngine(topo, params, R)
+    eng.reset(0)
+    out = compare_steady(oracle_mod, eng, topo, params, ("mlp", w), t_target_s=t_target, hops_per_launch=pr["hops"],
+                         min_episode=min_ep, net_cpu=net, log_tail=True,
+                         label=f"{preset} at the bench shape ({pr['hops']} hops, log {log_cap})")
+    eng.close()
+    assert out["t_compared_s"] >= t_target and min(out["episodes"]) >= min_ep and out["short_launches"] == 0
+
+
 def test_config3_abilene_on_geant_dqn_buffer_episode_end(oracle_mod):
     """Config 3 through the regime its bench runs in: the tunnelled-overlay kernels (relay entries
     with the tunnel target, LDS FIFO windows, engine_core.h q_put / q_take) from t = 0 past the 60-s
