@@ -361,6 +361,9 @@ struct Sim {
     const CAS uint32_t* m_fseq;
     const CAS BigSig* m_bs;
     uint32_t* lrec;                         // link records [L][kLRec] (HBM)
+    // issue priority by launch progress (prio_update): hops of the whole launch (0: off), hops done
+    // before this event loop, and the loop's hop count at which the priority next drops
+    uint32_t prio_total, prio_base, prio_next;
 #if PRISMA_TIMING
     mutable uint64_t tsub[2], tlast;             // sub-phase cycles inside apply_decision
     mutable uint64_t tmlp[4];                    // mlp_action phases (timing build)
@@ -406,6 +409,34 @@ __device__ inline void sim_bind(Sim& S, const LV& L, unsigned char* lds, const u
     S.ctrl = true;
     S.mlp_inst = false;
     S.lrec = nullptr;
+    S.prio_total = 0; S.prio_base = 0; S.prio_next = 0xffffffffu;
+}
+
+// Issue priority by launch progress.  A SIMD arbitrates its waves' issue by priority, then age
+// (MI355X_MICROARCH.md, two waves per SIMD), so at equal priority the oldest of a SIMD's 4
+// replicas runs ahead and the youngest finishes alone: measured on the headline
+// (scripts/wave_times.py), the 4 waves of a SIMD ended at about 89, 113, 124 and 146 ms of a
+// 146-ms launch, the last ~22 ms with one wave left to hide its own latency.  Here a wave's priority
+// drops as its share of the launch's hops is done (3 below 5/8, 2 below 13/16, 1 below 15/16, then 0),
+// so a wave that is ahead yields issue to the ones behind it and the SIMD keeps all four to the end.
+#ifndef PRISMA_PRIO
+#define PRISMA_PRIO 1
+#endif
+// (round-6 A/B on one box, profiles/r06_ab/ab_prio.txt: thresholds 5/8, 13/16, 15/16 +13.4 % at
+// the headline and +8.9 % at config 3; 1/2, 3/4, 7/8 (PRISMA_PRIO=2) +13.2 %; 1/4, 1/2, 3/4 +10 %;
+// 7/8, 15/16, 31/32 +4.5 %; a least-progress-first rank over the SIMD's four waves, exchanged
+// through global memory every 64 or 256 hops, -2 %)
+__device__ __forceinline__ void prio_update(Sim& S, uint32_t hops_loop) {
+    const uint32_t T = S.prio_total, p = S.prio_base + hops_loop;
+    uint32_t t1, t2, t3;
+    if (PRISMA_PRIO == 2) { t1 = T / 2; t2 = T - T / 4; t3 = T - T / 8; }
+    else { t1 = T / 2 + T / 8; t2 = T - T / 8 - T / 16; t3 = T - T / 16; }
+    uint32_t next;
+    if (p < t1) { __builtin_amdgcn_s_setprio(3); next = t1; }
+    else if (p < t2) { __builtin_amdgcn_s_setprio(2); next = t2; }
+    else if (p < t3) { __builtin_amdgcn_s_setprio(1); next = t3; }
+    else { __builtin_amdgcn_s_setprio(0); next = 0xffffffffu; }
+    S.prio_next = next == 0xffffffffu ? next : next - S.prio_base;
 }
 
 // Topology reads.  The register-resident engine reads the fixed-offset TopoImage,
@@ -2541,6 +2572,7 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
 
     H.stop = 0;
     H.hops_launch = 0;
+    if (PRISMA_PRIO && S.prio_total) prio_update(S, 0u);
     if (H.pend && !H.over) {
         if (table_mode) {
             uint32_t pn = u_ld32(&S.h->pend_node), pd = u_ld32(&S.h->pend_ent[1]);
@@ -2620,6 +2652,7 @@ __device__ __forceinline__ uint32_t event_loop(const KParams& P, Sim& S, RS& R, 
                                    D.r0, D.deg);
                     H.hops_launch++;
                     if (H.hops_launch >= max_hops) H.stop = 1;
+                    if (PRISMA_PRIO && H.hops_launch == S.prio_next) prio_update(S, H.hops_launch);
                     TM_MARK(2);
                 } else {
                     if (lane == 0) {

@@ -6,3 +6,4 @@
 const void* prisma_pick_step_lite(int fs, int ls, bool tun) { return pick_step<false, false>(fs, ls, tun); }
 
 PRISMA_TU_TIMING(prisma_debug_timing_lite)
+PRISMA_TU_WAVE_TIMES(prisma_debug_wave_times_lite)

@@ -26,11 +26,31 @@ template <int FS, int LS> struct StepOcc {
 // MLP: the in-kernel DQN-buffer policy is compiled in (mode 4 only); the table /
 // external instances carry none of its code or registers.  CTRL: the --train echo and
 // notify_dest paths are compiled in (used when either is set).
+#if PRISMA_WAVE_TIMES
+// diagnostic build only (scripts/wave_times.py): each replica's wave start / end (s_memrealtime,
+// 100 MHz) and hardware ids of its last launch
+__device__ unsigned long long g_wave_times[4 * 65536];
+#define WT_START() const uint64_t wt0_ = __builtin_amdgcn_s_memrealtime()
+#define WT_END()                                                                                       \
+    do {                                                                                               \
+        const uint64_t wt1_ = __builtin_amdgcn_s_memrealtime();                                        \
+        if (lane == 0 && r < 65536) {                                                                  \
+            g_wave_times[4 * r] = wt0_; g_wave_times[4 * r + 1] = wt1_;                                \
+            g_wave_times[4 * r + 2] = (unsigned)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)); \
+            g_wave_times[4 * r + 3] = (unsigned)__builtin_amdgcn_s_getreg((20) | (0 << 6) | (15 << 11)); \
+        }                                                                                              \
+    } while (0)
+#else
+#define WT_START() do { } while (0)
+#define WT_END() do { } while (0)
+#endif
+
 template <int FS, int LS, bool MLP, bool TUN, bool CTRL>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(StepOcc<FS, LS>::waves)))
 prisma_step_kernel_t(KParams P) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const int r = blockIdx.x, lane = threadIdx.x;
+    WT_START();
     CLayout& LC = *(CLayout*)P.lay;
     LV lv;
     lv.load(P.lay, lane);
@@ -43,6 +63,8 @@ prisma_step_kernel_t(KParams P) {
     S.ctrl = CTRL;
     if (TUN) S.ring = (uint32_t*)(P.state + (size_t)r * LC.state_bytes + LC.s_ring);   // HBM FIFOs
     uint32_t budget = (uint32_t)P.max_hops;
+    // (4-wave instances only: at 2 waves per SIMD, config 4's, the same thresholds lost 2 %)
+    S.prio_total = StepOcc<FS, LS>::waves >= 4 ? budget : 0u;
     const uint32_t done = event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P, S, R, r, budget);
     // an episode ended with hop budget left (fused run with auto_reset): the next episode from
     // its prebuilt image, in a second inlined copy of the event loop.  A restart inside the first
@@ -55,15 +77,18 @@ prisma_step_kernel_t(KParams P) {
         asm volatile("" : "+s"(kp));
         const KParams P2 = *kp;
         if (spare_restart(P2, S, R, r, done, budget)) {
+            S.prio_base = done;
             event_loop<MLP, StepOcc<FS, LS>::mlp_batch>(P2, S, R, r, budget);
             // stage out from the reloaded arguments too: with P's pointers kept live across this
             // loop the headline instance spilled 7 VGPRs and reloaded them inside it (round 6:
             // 128 VGPRs + 32 B scratch -> 123 VGPRs, no scratch)
             stage_out(lds, P2, r, lane, R);
+            WT_END();
             return;
         }
     }
     stage_out(lds, P, r, lane, R);
+    WT_END();
 }
 
 // instantiations: flow slots FS in {1,2,4,8} (F <= 512), link slots LS in {1,2,4} (L <= 256)
@@ -89,6 +114,16 @@ static const void* pick_step(int fs, int ls, bool tun) {
     return nullptr;
 #endif
 }
+
+#if PRISMA_WAVE_TIMES
+#define PRISMA_TU_WAVE_TIMES(NAME)                                                                      \
+    extern "C" int NAME(unsigned long long* out, int n) {                                               \
+        return (hipDeviceSynchronize() == hipSuccess &&                                                 \
+                hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wave_times), 4 * sizeof(unsigned long long) * n) == hipSuccess) ? 0 : -1; \
+    }
+#else
+#define PRISMA_TU_WAVE_TIMES(NAME)
+#endif
 
 #if PRISMA_TIMING
 // diagnostic build only: read and clear this translation unit's per-phase cycle totals
